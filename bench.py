@@ -1,0 +1,198 @@
+#!/usr/bin/env python3
+"""Benchmark: device-resident SHA-1 over 512 KiB chunks (BASELINE.json metric).
+
+One step = one pass of the hot path (SHA1Guts over every block of every
+chunk, sha.c:176-451, as shahash does per chunk, chunk.c:35-51) over one
+batch of synthetic chunks already resident in HBM.  Default workload =
+BASELINE config 2: 4096 x 524288 B per GPU.  Multi-GPU (torchrun, one rank
+per GPU): every rank hashes its own 4096 chunks (global chunk ids
+4096*rank ..), no data-path collective -> weak scaling; the only
+collectives are the timing barrier and the max-over-ranks reduction.
+
+Prints ONE JSON line on rank 0 with `roofline` (dominant kernel vs the HBM
+peak, per-launch time from HIP events on the kernel's own stream) and
+`cpu_baseline` (the reference sha.c, compiled from its sources into
+oracle/_ref, timed on this host's cores on the same chunks).
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "GiB/s device-resident SHA-1 over 512KB chunks; % of HBM-read roofline"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+VALU_OPS_PER_BLOCK = 613  # gfx950 ISA count per 64-B compression
+VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CU x 4 SIMD32 x 2.4 GHz lane-ops
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--chunks", type=int, default=4096, help="chunks per GPU")
+    ap.add_argument("--chunk-len", type=int, default=524288)
+    ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "fused", "split"])
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    pkg = importlib.import_module("congestion-control-with-bittorren_amd")
+    pkg.set_device(local)
+
+    n, L = a.chunks, a.chunk_len
+    first = rank * n  # weak scaling: each rank its own chunk ids
+    buf = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+    dig = torch.zeros((n, 20), dtype=torch.uint8, device="cuda")
+    stream = torch.cuda.Stream()
+    with torch.cuda.stream(stream):
+        pkg.synth_fill_device(buf, first, n, L, stream=stream)
+    stream.synchronize()
+
+    def step(ev0=None, ev1=None):
+        if ev0 is not None:
+            ev0.record(stream)
+        pkg.hash_uniform_device(buf, L, n, dig, stream=stream, kernel=a.kernel)
+        if ev1 is not None:
+            ev1.record(stream)
+
+    for _ in range(a.warmup):
+        step()
+    stream.synchronize()
+
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(a.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        step(e0, e1)
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+    if world > 1:
+        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_ms = float(t[0]), float(t[1])
+
+    # ---- parity of the timed output (every rank, against the reference) ----
+    got = dig.cpu().numpy()
+    from oracle import oracle as O  # checker only
+    golden = json.load(open(os.path.join(ROOT, "tests/golden/golden.json")))
+    parity = None
+    if n == 4096 and L == O.CHUNK_LEN and rank < len(golden["weak4096"]):
+        parity = O.digest_of_digests(got).hex() == golden["weak4096"][rank]
+    else:
+        idx = np.unique(np.linspace(0, n - 1, min(n, 16)).astype(np.int64))
+        host = np.concatenate([O.synth_chunks(first + int(i), 1, L) for i in idx])
+        want = O.hash_batch(host, np.arange(idx.size, dtype=np.uint64) * L,
+                            np.full(idx.size, L, np.uint32))
+        parity = bool(np.array_equal(got[idx], want))
+    if world > 1:
+        ok = torch.tensor([1.0 if parity else 0.0], device="cuda")
+        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+        parity = bool(ok.item() > 0.5)
+
+    ms_per_step = elapsed / a.steps * 1e3
+    total_bytes = world * n * L
+    value = total_bytes / (elapsed / a.steps) / 2**30
+    alg_bytes = n * (L + 20)  # per launch: every chunk byte read once + its digest
+    achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
+    blocks = n * ((L + 8) // 64 + 1)
+    valu_tops = blocks * 64 * VALU_OPS_PER_BLOCK / (kern_ms * 1e-3) / 1e12
+
+    result = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "GiB/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic (splitmix64 corpus, SURVEY.md 8d), resident in HBM",
+        "config": {"workload": f"{n} x {L} B chunks per GPU, device-resident (BASELINE config 2)",
+                   "chunks_per_gpu": n, "chunk_bytes": L, "kernel": a.kernel,
+                   "parallelism": f"chunk-sharded x{world}, no collective"},
+        "parity": parity,
+        "roofline": {
+            "bound": "hbm",
+            "achieved": round(achieved, 2),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 5),
+            "traffic": _traffic(n, L),
+            "kernel_ms": round(kern_ms, 4),
+            "valu": {"achieved_tops": round(valu_tops, 3), "peak_tops": round(VALU_PEAK_TOPS, 2),
+                     "frac": round(valu_tops / VALU_PEAK_TOPS, 5),
+                     "ops_per_block": VALU_OPS_PER_BLOCK},
+        },
+    }
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        result["cpu_baseline"] = _cpu_baseline(O, n, L, a.cpu_threads, golden)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def _traffic(n: int, L: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC pass (FETCH_SIZE
+    x2 gfx950 correction + WRITE_SIZE), if one was recorded for this shape."""
+    for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "*traffic*.json")), reverse=True):
+        try:
+            rec = json.load(open(path))
+        except Exception:
+            continue
+        if rec.get("chunks") == n and rec.get("chunk_bytes") == L and "bytes_per_launch" in rec:
+            return rec["bytes_per_launch"]
+    return None
+
+
+def _cpu_baseline(O, n, L, threads, golden):
+    """The reference sha.c (oracle/_ref, -O2) on this host's cores over the
+    same synthetic chunks (a bounded sample of up to 4096 chunks)."""
+    sample = min(n, 4096)
+    kind = "reference" if O.ref_lib() is not None else "port"
+    threads = max(1, min(threads, os.cpu_count() or 1))
+    secs, agg = O.time_synth(sample, L, threads=threads, kind=kind)
+    same = None
+    if sample == 4096 and L == O.CHUNK_LEN:
+        same = agg.hex() == golden["weak4096"][0]
+    return {"value": round(sample * L / secs / 2**30, 3), "unit": "GiB/s", "cores": threads,
+            "kind": kind,
+            "sample": f"chunks 0..{sample - 1} x {L} B of the same corpus, -O2, "
+                      f"{threads} pthreads chunk-strided; digests match reference golden: {same}"}
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,215 @@
+// sha1_device.hpp -- SHA-1 compression for gfx950 (CDNA4), device side.
+//
+// What the reference computes (file:line in /root/reference):
+//   SHA1Guts      sha.c:176-451  one compression of a 64-byte block
+//     BE load     sha.c:186-189  W[0..15] = byte-swapped input words
+//     schedule    sha.c:191-200  W[t] = ROTL1(W[t-3]^W[t-8]^W[t-14]^W[t-16])
+//     rounds      sha.c:57-69    temp = ROTL5(a)+F(b,c,d)+e+W+K, c = ROTL30(b)
+//     feed-fwd    sha.c:446-450  hash[i] += a..e
+//   SHA1Final     sha.c:529-558  0x80 pad to 56 mod 64, 64-bit BE bit count
+//
+// How it maps to CDNA4 (one SHA-1 message per lane; 64 messages per wave):
+//   rotate            -> v_alignbit_b32 (1 op)
+//   Ch                -> v_bfi_b32 (compiler pattern)  Parity/Maj -> v_bitop3_b32
+//   5-term round sum  -> 2 x v_add3_u32
+//   schedule xor4     -> v_bitop3_b32(xor3) + v_xor_b32, then v_alignbit_b32
+//   byte swap         -> v_perm_b32
+// = ~613 VALU per 64-byte block, no MFMA, no LDS inside the compression.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace s1 {
+
+constexpr uint32_t K0 = 0x5a827999u, K1 = 0x6ed9eba1u, K2 = 0x8f1bbcdcu, K3 = 0xca62c1d6u;
+constexpr uint32_t IV0 = 0x67452301u, IV1 = 0xefcdab89u, IV2 = 0x98badcfeu, IV3 = 0x10325476u,
+                   IV4 = 0xc3d2e1f0u;
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, uint32_t s) {
+    return __builtin_amdgcn_alignbit(x, x, 32u - s);
+}
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
+}
+__device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
+    return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
+}
+__device__ __forceinline__ uint32_t chf(uint32_t b, uint32_t c, uint32_t d) {
+    return d ^ (b & (c ^ d));  // -> v_bfi_b32
+}
+__device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+
+// Round t (compile-time after unrolling) over the five-word state v[], kept
+// in place: a = v[(0-t)%5] ... e = v[(4-t)%5]; the new a lands in e's slot
+// and b is rotated in its own slot, so no register moves are emitted.
+template <int T>
+__device__ __forceinline__ void round_step(uint32_t (&v)[5], uint32_t wt) {
+    constexpr int ia = (5 - (T % 5)) % 5;
+    constexpr int ib = (ia + 1) % 5, ic = (ia + 2) % 5, id = (ia + 3) % 5, ie = (ia + 4) % 5;
+    uint32_t f, k;
+    if constexpr (T < 20) {
+        f = chf(v[ib], v[ic], v[id]);
+        k = K0;
+    } else if constexpr (T < 40) {
+        f = xor3(v[ib], v[ic], v[id]);
+        k = K1;
+    } else if constexpr (T < 60) {
+        f = maj(v[ib], v[ic], v[id]);
+        k = K2;
+    } else {
+        f = xor3(v[ib], v[ic], v[id]);
+        k = K3;
+    }
+    v[ie] = v[ie] + rotl(v[ia], 5) + f + k + wt;
+    v[ib] = rotl(v[ib], 30);
+}
+
+// In-place 16-word window expansion for round T >= 16.
+template <int T>
+__device__ __forceinline__ uint32_t sched_step(uint32_t (&w)[16]) {
+    uint32_t x = rotl(xor3(w[(T - 3) & 15], w[(T - 8) & 15], w[(T - 14) & 15]) ^ w[T & 15], 1);
+    w[T & 15] = x;
+    return x;
+}
+
+template <int T>
+struct Rounds {
+    __device__ __forceinline__ static void run(uint32_t (&v)[5], uint32_t (&w)[16]) {
+        uint32_t wt;
+        if constexpr (T < 16)
+            wt = w[T];
+        else
+            wt = sched_step<T>(w);
+        round_step<T>(v, wt);
+        Rounds<T + 1>::run(v, w);
+    }
+};
+template <>
+struct Rounds<80> {
+    __device__ __forceinline__ static void run(uint32_t (&)[5], uint32_t (&)[16]) {}
+};
+
+// One full compression: h[] <- h[] + F(h[], w[]); w[] holds the block as
+// big-endian words and is consumed (overwritten by the schedule).
+__device__ __forceinline__ void compress(uint32_t (&h)[5], uint32_t (&w)[16]) {
+    uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
+    Rounds<0>::run(v, w);
+#pragma unroll
+    for (int i = 0; i < 5; ++i) h[i] += v[i];
+}
+
+// Rounds only, with the 80-word schedule supplied in registers (split
+// kernel consumer: the producer wave computed it).
+template <int T>
+struct RoundsW {
+    __device__ __forceinline__ static void run(uint32_t (&v)[5], const uint32_t (&W)[80]) {
+        round_step<T>(v, W[T]);
+        RoundsW<T + 1>::run(v, W);
+    }
+};
+template <>
+struct RoundsW<80> {
+    __device__ __forceinline__ static void run(uint32_t (&)[5], const uint32_t (&)[80]) {}
+};
+
+// Padding of the final partial block (sha.c:536-543): word i of the block
+// holds message bytes [4i, 4i+4) as a big-endian word; keep the first
+// `rem` bytes of the block, put 0x80 right after them, zero the rest.
+__device__ __forceinline__ uint32_t pad_word(uint32_t w, int i, int rem) {
+    const int valid = rem - 4 * i;  // message bytes of this word still in the block
+    if (valid >= 4) return w;
+    if (valid < 0) return 0u;
+    const uint32_t keep = valid == 0 ? 0u : (0xffffffffu << (32 - 8 * valid));
+    return (w & keep) | (0x80000000u >> (8 * valid));
+}
+
+__device__ __forceinline__ void init_state(uint32_t (&h)[5]) {
+    h[0] = IV0;
+    h[1] = IV1;
+    h[2] = IV2;
+    h[3] = IV3;
+    h[4] = IV4;
+}
+
+// ---------------------------------------------------------------------------
+// Per-lane loads from global memory (any byte alignment).  `p` points at the
+// first byte of the block, `avail` is how many message bytes remain from p
+// (>= 64 for a full block).  Reads never touch a 4-byte word that holds no
+// message byte, so they never cross into an unmapped page.  Output: the
+// block's words as LITTLE-endian loads (byte-swap is done by the caller).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void load_block_full(const uint8_t* p, uint32_t (&w)[16]) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    if ((a & 15u) == 0) {
+        const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint4 x = q[j];
+            w[4 * j + 0] = x.x;
+            w[4 * j + 1] = x.y;
+            w[4 * j + 2] = x.z;
+            w[4 * j + 3] = x.w;
+        }
+    } else {
+        const uint32_t sh = static_cast<uint32_t>(a & 3u);
+        const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+        uint32_t d[17];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) d[j] = q[j];
+        d[16] = sh ? q[16] : 0u;
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+    }
+}
+
+__device__ __forceinline__ void load_block_partial(const uint8_t* p, uint32_t avail,
+                                                   uint32_t (&w)[16]) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t sh = static_cast<uint32_t>(a & 3u);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+    const uint32_t span = avail + sh;  // bytes from the aligned base to the message end
+    uint32_t d[17];
+#pragma unroll
+    for (int j = 0; j < 17; ++j) d[j] = (uint32_t)(4 * j) < span ? q[j] : 0u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+}
+
+// Final block(s) of a message whose last `rem` (< 64) bytes start at p.
+// Compresses one or two padded blocks into h.  total_bytes is the whole
+// message length (prefix + this call), used for the 64-bit bit count.
+__device__ __forceinline__ void finish_message(uint32_t (&h)[5], const uint8_t* p, uint32_t rem,
+                                               uint64_t total_bytes) {
+    uint32_t w[16];
+    if (rem) {
+        load_block_partial(p, rem, w);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = pad_word(bswap(w[j]), j, static_cast<int>(rem));
+    const uint64_t bits = total_bytes * 8ull;
+    const uint32_t hi = static_cast<uint32_t>(bits >> 32), lo = static_cast<uint32_t>(bits);
+    if (rem < 56) {
+        w[14] = hi;
+        w[15] = lo;
+        compress(h, w);
+    } else {
+        compress(h, w);
+#pragma unroll
+        for (int j = 0; j < 14; ++j) w[j] = 0u;
+        w[14] = hi;
+        w[15] = lo;
+        compress(h, w);
+    }
+}
+
+__device__ __forceinline__ void store_digest(uint8_t* out, const uint32_t (&h)[5]) {
+    uint32_t* o = reinterpret_cast<uint32_t*>(out);  // 4-byte aligned (checked on host)
+#pragma unroll
+    for (int i = 0; i < 5; ++i) o[i] = bswap(h[i]);
+}
+
+}  // namespace s1

@@ -1,0 +1,30 @@
+// sha1_kernels.h -- kernel arguments and launchers (internal to libsha1chunk).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+// One batch of independent messages.  Message e (0 <= e < n) is chunk
+// id = order ? order[e] : e, bytes base[off[id] .. off[id] + len[id]),
+// with off/len replaced by id*ulen / ulen when the arrays are null.
+struct BatchArgs {
+    const uint8_t* base;
+    const uint64_t* off;
+    const uint32_t* len;
+    uint32_t ulen;
+    uint32_t n;
+    const uint32_t* order;
+    uint8_t* dig;  // n x 20 digest bytes (finalising mode), 4-byte aligned
+    // Streaming extras (lane kernel only; null/0 for plain batches):
+    const uint32_t* init_state;  // 5 words per message instead of the IV
+    uint64_t prefix_bytes;       // bytes already hashed before this call
+    uint32_t* out_state;         // non-null: no padding, write raw state
+};
+
+hipError_t launch_lane(const BatchArgs& A, hipStream_t st);
+hipError_t launch_fused(const BatchArgs& A, hipStream_t st);
+hipError_t launch_split(const BatchArgs& A, hipStream_t st);
+hipError_t launch_synth(uint8_t* dst, const uint64_t* off, const uint32_t* lens, uint32_t ulen,
+                        uint64_t first, uint64_t count, uint64_t seed, hipStream_t st);
+hipError_t launch_compare(const uint8_t* dig, const uint8_t* exp, uint32_t n, uint8_t* mismatch,
+                          hipStream_t st);

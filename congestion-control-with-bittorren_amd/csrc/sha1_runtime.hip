@@ -1,0 +1,626 @@
+// sha1_runtime.hip -- host runtime of libsha1chunk.so: the C-ABI batch entry
+// points of include/sha1chunk.h.
+//
+// Per device: one compute stream per pipeline slot, a device arena and a
+// pinned host arena for each of two slots, so that packing/reading batch b+1
+// on the host, its H2D copy, the kernel of batch b and the D2H of digests
+// overlap.  Everything that hashes runs on the GPU; the host only moves
+// bytes and bookkeeping (sorting by length, packing, scattering digests).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cerrno>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <thread>
+#include <unistd.h>
+#include <vector>
+
+#include "../../include/sha1chunk.h"
+#include "sha1_kernels.h"
+
+namespace {
+
+thread_local std::string t_err;
+thread_local int t_dev = 0;
+
+int fail(int code, const char* fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    t_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                         \
+    do {                                                                                      \
+        hipError_t e_ = (expr);                                                               \
+        if (e_ != hipSuccess)                                                                 \
+            return fail(SHA1CHUNK_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                        __FILE__, __LINE__);                                                  \
+    } while (0)
+
+constexpr size_t kAlign = 128;  // device layout: every chunk starts on a 128-B line
+constexpr size_t kSlotBytes = size_t(256) << 20;  // host-batch pipeline slot (256 MiB)
+
+inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return SHA1CHUNK_OK;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        bytes = round_up(std::max(bytes, size_t(1) << 20), size_t(1) << 20);
+        if (hipMalloc(&p, bytes) != hipSuccess)
+            return fail(SHA1CHUNK_ENOMEM, "hipMalloc(%zu) failed", bytes);
+        cap = bytes;
+        return SHA1CHUNK_OK;
+    }
+};
+
+struct PinBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t bytes) {
+        if (bytes <= cap) return SHA1CHUNK_OK;
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+        bytes = round_up(std::max(bytes, size_t(1) << 20), size_t(1) << 20);
+        if (hipHostMalloc(&p, bytes, hipHostMallocDefault) != hipSuccess)
+            return fail(SHA1CHUNK_ENOMEM, "hipHostMalloc(%zu) failed", bytes);
+        cap = bytes;
+        return SHA1CHUNK_OK;
+    }
+};
+
+// One pipeline slot: pinned staging for [meta | data], device mirror,
+// digests on both sides, its own stream and completion event.
+struct Slot {
+    PinBuf hpin;    // meta (offsets, lengths, order) then chunk bytes
+    PinBuf hdig;    // n x 20 digests back from the device
+    DevBuf dmem;    // device copy of hpin
+    DevBuf ddig;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    bool busy = false;
+    // bookkeeping for the batch in flight
+    std::vector<uint32_t> ids;  // caller chunk index of each staged entry
+};
+
+struct Device {
+    std::mutex mu;
+    bool ready = false;
+    int id = -1;
+    int cus = 256;
+    Slot slot[2];
+    DevBuf small;  // streaming calls: state + data
+    PinBuf small_pin;
+};
+
+std::once_flag g_once;
+int g_count = -1;  // >= 0 once probed
+std::string g_probe_err;
+Device* g_dev = nullptr;
+
+void probe() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) {
+        g_count = 0;
+        g_probe_err = "no HIP device visible";
+        return;
+    }
+    int ok = 0;
+    for (int d = 0; d < n; ++d) {
+        hipDeviceProp_t pr;
+        if (hipGetDeviceProperties(&pr, d) != hipSuccess) continue;
+        if (strncmp(pr.gcnArchName, "gfx950", 6) != 0) {
+            g_probe_err = std::string("device ") + std::to_string(d) + " is " + pr.gcnArchName +
+                          ", this build targets gfx950 only";
+            continue;
+        }
+        ++ok;
+    }
+    if (ok != n) {
+        g_count = 0;
+        return;
+    }
+    g_count = n;
+    g_dev = new Device[n];
+    for (int d = 0; d < n; ++d) g_dev[d].id = d;
+}
+
+int device_count() {
+    std::call_once(g_once, probe);
+    return g_count;
+}
+
+// Acquire the calling thread's device (initialising it on first use).
+int get_device(Device** out) {
+    if (device_count() <= 0) return fail(SHA1CHUNK_ENODEV, "%s", g_probe_err.c_str());
+    if (t_dev < 0 || t_dev >= g_count) return fail(SHA1CHUNK_EINVAL, "bad device %d", t_dev);
+    Device& D = g_dev[t_dev];
+    HIP_TRY(hipSetDevice(D.id));
+    if (!D.ready) {
+        std::lock_guard<std::mutex> lk(D.mu);
+        if (!D.ready) {
+            hipDeviceProp_t pr;
+            HIP_TRY(hipGetDeviceProperties(&pr, D.id));
+            D.cus = pr.multiProcessorCount;
+            for (auto& s : D.slot) {
+                HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+                HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+            }
+            D.ready = true;
+        }
+    }
+    *out = &D;
+    return SHA1CHUNK_OK;
+}
+
+// Pick the kernel for a batch of n chunks on a device with `cus` CUs.  The
+// split kernel halves each chunk's serial instruction stream but needs two
+// waves per 64 chunks; once there are enough chunks to give every SIMD two
+// waves of its own, the fused kernel does the same work with less LDS traffic.
+int choose_kernel(int kernel, size_t n, int cus) {
+    if (kernel != SHA1CHUNK_KERNEL_AUTO) return kernel;
+    const size_t groups = (n + 63) / 64;
+    return groups <= size_t(cus) * 4 ? SHA1CHUNK_KERNEL_SPLIT : SHA1CHUNK_KERNEL_FUSED;
+}
+
+hipError_t launch(int kernel, const BatchArgs& A, hipStream_t st) {
+    switch (kernel) {
+    case SHA1CHUNK_KERNEL_LANE: return launch_lane(A, st);
+    case SHA1CHUNK_KERNEL_FUSED: return launch_fused(A, st);
+    case SHA1CHUNK_KERNEL_SPLIT: return launch_split(A, st);
+    default: return hipErrorInvalidValue;
+    }
+}
+
+int launch_checked(int kernel, const BatchArgs& A, hipStream_t st) {
+    if (kernel < SHA1CHUNK_KERNEL_LANE || kernel > SHA1CHUNK_KERNEL_SPLIT)
+        return fail(SHA1CHUNK_EINVAL, "unknown kernel id %d", kernel);
+    if (A.n > 0 && (reinterpret_cast<uintptr_t>(A.dig) & 3u))
+        return fail(SHA1CHUNK_EALIGN, "digest buffer must be 4-byte aligned");
+    hipError_t e = launch(kernel, A, st);
+    if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "kernel launch: %s", hipGetErrorString(e));
+    return SHA1CHUNK_OK;
+}
+
+// ------------------------------------------------------------ host batch --
+// Stage entries [lo, hi) of `order` (caller indices, sorted by length) into
+// slot s and launch.  Layout in the pinned / device buffer:
+//   [off: u64 x m][len: u32 x m] pad to 128 | chunk bytes (each 128-aligned)
+int stage_and_launch(Device& D, Slot& s, const uint8_t* base, const uint64_t* offsets,
+                     const uint32_t* lengths, const std::vector<uint32_t>& order, size_t lo,
+                     size_t hi, size_t data_bytes) {
+    const size_t m = hi - lo;
+    const size_t meta = round_up(m * (sizeof(uint64_t) + sizeof(uint32_t)), kAlign);
+    int rc;
+    if ((rc = s.hpin.ensure(meta + data_bytes)) || (rc = s.dmem.ensure(meta + data_bytes)) ||
+        (rc = s.hdig.ensure(m * 20)) || (rc = s.ddig.ensure(m * 20)))
+        return rc;
+    uint8_t* h = static_cast<uint8_t*>(s.hpin.p);
+    uint64_t* hoff = reinterpret_cast<uint64_t*>(h);
+    uint32_t* hlen = reinterpret_cast<uint32_t*>(h + m * sizeof(uint64_t));
+    s.ids.assign(order.begin() + lo, order.begin() + hi);
+    size_t cur = meta;
+    for (size_t j = 0; j < m; ++j) {
+        const uint32_t id = s.ids[j];
+        const uint32_t L = lengths[id];
+        hoff[j] = cur;
+        hlen[j] = L;
+        if (L) memcpy(h + cur, base + offsets[id], L);
+        cur += round_up(L, kAlign);
+    }
+    HIP_TRY(hipMemcpyAsync(s.dmem.p, h, cur, hipMemcpyHostToDevice, s.stream));
+    uint8_t* d = static_cast<uint8_t*>(s.dmem.p);
+    BatchArgs A{};
+    A.base = d;
+    A.off = reinterpret_cast<const uint64_t*>(d);
+    A.len = reinterpret_cast<const uint32_t*>(d + m * sizeof(uint64_t));
+    A.n = static_cast<uint32_t>(m);
+    A.dig = static_cast<uint8_t*>(s.ddig.p);
+    // Offsets in the staged buffer are relative to its start; entries are
+    // already in length order, so no order[] indirection is needed.
+    if ((rc = launch_checked(choose_kernel(SHA1CHUNK_KERNEL_AUTO, m, D.cus), A, s.stream)))
+        return rc;
+    HIP_TRY(hipMemcpyAsync(s.hdig.p, s.ddig.p, m * 20, hipMemcpyDeviceToHost, s.stream));
+    HIP_TRY(hipEventRecord(s.done, s.stream));
+    s.busy = true;
+    return SHA1CHUNK_OK;
+}
+
+int drain(Slot& s, uint8_t* digests) {
+    if (!s.busy) return SHA1CHUNK_OK;
+    s.busy = false;
+    HIP_TRY(hipEventSynchronize(s.done));
+    const uint8_t* src = static_cast<const uint8_t*>(s.hdig.p);
+    for (size_t j = 0; j < s.ids.size(); ++j) memcpy(digests + 20ull * s.ids[j], src + 20 * j, 20);
+    return SHA1CHUNK_OK;
+}
+
+int hash_host(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths, size_t n,
+              uint8_t* digests) {
+    Device* D;
+    int rc = get_device(&D);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(D->mu);
+    // Longest first, so every wave of 64 gets near-equal lengths (a wave
+    // runs as long as its longest lane).
+    std::vector<uint32_t> order(n);
+    std::iota(order.begin(), order.end(), 0u);
+    std::stable_sort(order.begin(), order.end(),
+                     [&](uint32_t a, uint32_t b) { return lengths[a] > lengths[b]; });
+    size_t lo = 0;
+    int which = 0;
+    while (lo < n) {
+        size_t hi = lo, bytes = 0;
+        while (hi < n) {
+            const size_t b = round_up(lengths[order[hi]], kAlign);
+            if (hi > lo && bytes + b > kSlotBytes) break;
+            bytes += b;
+            ++hi;
+        }
+        Slot& s = D->slot[which];
+        if ((rc = drain(s, digests))) return rc;
+        if ((rc = stage_and_launch(*D, s, base, offsets, lengths, order, lo, hi, bytes))) return rc;
+        lo = hi;
+        which ^= 1;
+    }
+    if ((rc = drain(D->slot[which], digests))) return rc;
+    return drain(D->slot[which ^ 1], digests);
+}
+
+// Shard a host batch over every device: contiguous, byte-balanced slices,
+// one host thread per device, no collective.
+int hash_host_all(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths, size_t n,
+                  uint8_t* digests) {
+    const int nd = device_count();
+    if (nd <= 0) return fail(SHA1CHUNK_ENODEV, "%s", g_probe_err.c_str());
+    if (nd == 1 || n < 64) return hash_host(base, offsets, lengths, n, digests);
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; ++i) total += lengths[i];
+    std::vector<size_t> cut(nd + 1, n);
+    cut[0] = 0;
+    uint64_t acc = 0;
+    int d = 1;
+    for (size_t i = 0; i < n && d < nd; ++i) {
+        acc += lengths[i];
+        while (d < nd && acc >= total * (uint64_t)d / (uint64_t)nd) cut[d++] = i + 1;
+    }
+    std::vector<int> rcs(nd, 0);
+    std::vector<std::string> errs(nd);
+    std::vector<std::thread> th;
+    for (int g = 0; g < nd; ++g) {
+        th.emplace_back([&, g] {
+            t_dev = g;
+            const size_t a = cut[g], b = cut[g + 1];
+            if (b > a) {
+                std::vector<uint64_t> off(offsets + a, offsets + b);
+                rcs[g] = hash_host(base, off.data(), lengths + a, b - a, digests + 20 * a);
+                if (rcs[g]) errs[g] = t_err;
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+    for (int g = 0; g < nd; ++g)
+        if (rcs[g]) return fail(rcs[g], "device %d: %s", g, errs[g].c_str());
+    return SHA1CHUNK_OK;
+}
+
+}  // namespace
+
+// ================================================================ C ABI ====
+extern "C" {
+
+int sha1chunk_device_count(void) {
+    const int n = device_count();
+    if (n <= 0) fail(SHA1CHUNK_ENODEV, "%s", g_probe_err.c_str());
+    return n;
+}
+
+int sha1chunk_set_device(int device) {
+    const int n = device_count();
+    if (n <= 0) return fail(SHA1CHUNK_ENODEV, "%s", g_probe_err.c_str());
+    if (device < 0 || device >= n) return fail(SHA1CHUNK_EINVAL, "device %d of %d", device, n);
+    t_dev = device;
+    return SHA1CHUNK_OK;
+}
+
+int sha1chunk_get_device(void) { return t_dev; }
+
+const char* sha1chunk_last_error(void) { return t_err.c_str(); }
+
+const char* sha1chunk_version(void) { return "sha1chunk gfx950: lane,fused,split"; }
+
+int sha1chunk_hash_device_async(const void* d_base, const uint64_t* d_offsets,
+                                const uint32_t* d_lengths, size_t n, uint8_t* d_digests,
+                                void* stream, int kernel) {
+    if (n > 0xffffffffu) return fail(SHA1CHUNK_EINVAL, "n too large");
+    if (n && (!d_base || !d_offsets || !d_lengths || !d_digests))
+        return fail(SHA1CHUNK_EINVAL, "null device pointer");
+    Device* D;
+    int rc = get_device(&D);
+    if (rc) return rc;
+    BatchArgs A{};
+    A.base = static_cast<const uint8_t*>(d_base);
+    A.off = d_offsets;
+    A.len = d_lengths;
+    A.n = static_cast<uint32_t>(n);
+    A.dig = d_digests;
+    return launch_checked(choose_kernel(kernel, n, D->cus), A, static_cast<hipStream_t>(stream));
+}
+
+int sha1chunk_hash_uniform_async(const void* d_base, uint32_t chunk_len, size_t n,
+                                 uint8_t* d_digests, void* stream, int kernel) {
+    if (n > 0xffffffffu) return fail(SHA1CHUNK_EINVAL, "n too large");
+    if (n && (!d_base || !d_digests)) return fail(SHA1CHUNK_EINVAL, "null device pointer");
+    Device* D;
+    int rc = get_device(&D);
+    if (rc) return rc;
+    BatchArgs A{};
+    A.base = static_cast<const uint8_t*>(d_base);
+    A.ulen = chunk_len;
+    A.n = static_cast<uint32_t>(n);
+    A.dig = d_digests;
+    return launch_checked(choose_kernel(kernel, n, D->cus), A, static_cast<hipStream_t>(stream));
+}
+
+int sha1chunk_compare_device_async(const uint8_t* d_digests, const uint8_t* d_expected, size_t n,
+                                   uint8_t* d_mismatch, void* stream) {
+    Device* D;
+    int rc = get_device(&D);
+    if (rc) return rc;
+    hipError_t e = launch_compare(d_digests, d_expected, static_cast<uint32_t>(n), d_mismatch,
+                                  static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "compare launch: %s", hipGetErrorString(e));
+    return SHA1CHUNK_OK;
+}
+
+int sha1chunk_hash_batch(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                         size_t n, uint8_t* digests, unsigned flags) {
+    if (n == 0) return SHA1CHUNK_OK;
+    if (!base || !offsets || !lengths || !digests) return fail(SHA1CHUNK_EINVAL, "null pointer");
+    if (n > 0xffffffffu) return fail(SHA1CHUNK_EINVAL, "n too large");
+    if (flags & SHA1CHUNK_DEVICE) {
+        Device* D;
+        int rc = get_device(&D);
+        if (rc) return rc;
+        std::lock_guard<std::mutex> lk(D->mu);
+        hipStream_t st = D->slot[0].stream;
+        if ((rc = sha1chunk_hash_device_async(base, offsets, lengths, n, digests, st,
+                                              SHA1CHUNK_KERNEL_AUTO)))
+            return rc;
+        HIP_TRY(hipStreamSynchronize(st));
+        return SHA1CHUNK_OK;
+    }
+    const uint8_t* b = static_cast<const uint8_t*>(base);
+    if (flags & SHA1CHUNK_ALL_DEVICES) return hash_host_all(b, offsets, lengths, n, digests);
+    return hash_host(b, offsets, lengths, n, digests);
+}
+
+int sha1chunk_verify_batch(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+                           size_t n, const uint8_t* expected, uint8_t* mismatch, unsigned flags) {
+    if (n == 0) return SHA1CHUNK_OK;
+    if (!expected || !mismatch) return fail(SHA1CHUNK_EINVAL, "null pointer");
+    if (flags & SHA1CHUNK_DEVICE) {
+        Device* D;
+        int rc = get_device(&D);
+        if (rc) return rc;
+        std::lock_guard<std::mutex> lk(D->mu);
+        Slot& s = D->slot[0];
+        if ((rc = s.ddig.ensure(n * 20))) return rc;
+        if ((rc = sha1chunk_hash_device_async(base, offsets, lengths, n,
+                                              static_cast<uint8_t*>(s.ddig.p), s.stream,
+                                              SHA1CHUNK_KERNEL_AUTO)))
+            return rc;
+        if ((rc = sha1chunk_compare_device_async(static_cast<uint8_t*>(s.ddig.p), expected, n,
+                                                 mismatch, s.stream)))
+            return rc;
+        HIP_TRY(hipStreamSynchronize(s.stream));
+        return SHA1CHUNK_OK;
+    }
+    std::vector<uint8_t> dig(n * 20);
+    int rc = sha1chunk_hash_batch(base, offsets, lengths, n, dig.data(), flags);
+    if (rc) return rc;
+    for (size_t i = 0; i < n; ++i) mismatch[i] = memcmp(&dig[20 * i], expected + 20 * i, 20) != 0;
+    return SHA1CHUNK_OK;
+}
+
+long sha1chunk_hash_stream(sha1chunk_reader_fn reader, void* reader_ctx, sha1chunk_sink_fn sink,
+                           void* sink_ctx) {
+    if (!reader) return fail(SHA1CHUNK_EINVAL, "null reader");
+    Device* D;
+    int rc = get_device(&D);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(D->mu);
+    const size_t per_slot = kSlotBytes / SHA1CHUNK_CHUNK_LEN;  // 512 chunks per slot
+    const size_t meta = round_up(per_slot * 12, kAlign);
+    size_t next = 0;  // index of the next slot's first chunk
+    size_t pend_first[2] = {0, 0}, pend_m[2] = {0, 0};
+    auto finish = [&](int w) -> int {
+        Slot& s = D->slot[w];
+        if (!s.busy) return SHA1CHUNK_OK;
+        s.busy = false;
+        HIP_TRY(hipEventSynchronize(s.done));
+        if (sink) sink(sink_ctx, pend_first[w], static_cast<const uint8_t*>(s.hdig.p), pend_m[w]);
+        return SHA1CHUNK_OK;
+    };
+    int which = 0;
+    bool eof = false;
+    while (!eof) {
+        Slot& s = D->slot[which];
+        if ((rc = finish(which))) return rc;
+        if ((rc = s.hpin.ensure(meta + kSlotBytes)) || (rc = s.dmem.ensure(meta + kSlotBytes)) ||
+            (rc = s.hdig.ensure(per_slot * 20)) || (rc = s.ddig.ensure(per_slot * 20)))
+            return rc;
+        uint8_t* h = static_cast<uint8_t*>(s.hpin.p);
+        // Read straight into pinned memory: the fread loop of make_chunks
+        // (chunk.c:22), a slot of 512 chunks at a time.
+        size_t got = 0;
+        while (got < kSlotBytes) {
+            const size_t r = reader(reader_ctx, h + meta + got, kSlotBytes - got);
+            if (r == (size_t)-1) return fail(SHA1CHUNK_EIO, "stream read error");
+            if (r == 0) {
+                eof = true;
+                break;
+            }
+            got += r;
+        }
+        if (got == 0) break;
+        const size_t m = (got + SHA1CHUNK_CHUNK_LEN - 1) / SHA1CHUNK_CHUNK_LEN;
+        uint64_t* hoff = reinterpret_cast<uint64_t*>(h);
+        uint32_t* hlen = reinterpret_cast<uint32_t*>(h + m * 8);
+        for (size_t j = 0; j < m; ++j) {
+            hoff[j] = meta + j * SHA1CHUNK_CHUNK_LEN;
+            hlen[j] = static_cast<uint32_t>(
+                std::min<size_t>(SHA1CHUNK_CHUNK_LEN, got - j * SHA1CHUNK_CHUNK_LEN));
+        }
+        HIP_TRY(hipMemcpyAsync(s.dmem.p, h, meta + got, hipMemcpyHostToDevice, s.stream));
+        uint8_t* d = static_cast<uint8_t*>(s.dmem.p);
+        BatchArgs A{};
+        A.base = d;
+        A.off = reinterpret_cast<const uint64_t*>(d);
+        A.len = reinterpret_cast<const uint32_t*>(d + m * 8);
+        A.n = static_cast<uint32_t>(m);
+        A.dig = static_cast<uint8_t*>(s.ddig.p);
+        if ((rc = launch_checked(choose_kernel(SHA1CHUNK_KERNEL_AUTO, m, D->cus), A, s.stream)))
+            return rc;
+        HIP_TRY(hipMemcpyAsync(s.hdig.p, s.ddig.p, m * 20, hipMemcpyDeviceToHost, s.stream));
+        HIP_TRY(hipEventRecord(s.done, s.stream));
+        s.busy = true;
+        pend_first[which] = next;
+        pend_m[which] = m;
+        next += m;
+        which ^= 1;
+    }
+    if ((rc = finish(which))) return rc;
+    if ((rc = finish(which ^ 1))) return rc;
+    return static_cast<long>(next);
+}
+
+namespace {
+struct FdSink {
+    uint8_t* out;
+    size_t max;
+};
+static size_t fd_reader(void* ctx, void* dst, size_t n) {
+    const int fd = *static_cast<int*>(ctx);
+    for (;;) {
+        const ssize_t r = read(fd, dst, n);
+        if (r >= 0) return static_cast<size_t>(r);
+        if (errno != EINTR) return (size_t)-1;
+    }
+}
+static void fd_sink(void* ctx, size_t first, const uint8_t* dig, size_t count) {
+    FdSink* s = static_cast<FdSink*>(ctx);
+    for (size_t j = 0; j < count; ++j)
+        if (first + j < s->max && s->out) memcpy(s->out + 20 * (first + j), dig + 20 * j, 20);
+}
+}  // namespace
+
+long sha1chunk_hash_fd(int fd, uint8_t* digests, size_t max_chunks, size_t* total_chunks) {
+    FdSink sk{digests, max_chunks};
+    const long n = sha1chunk_hash_stream(fd_reader, &fd, fd_sink, &sk);
+    if (n < 0) return n;
+    if (total_chunks) *total_chunks = static_cast<size_t>(n);
+    return static_cast<long>(std::min(static_cast<size_t>(n), max_chunks));
+}
+
+int sha1chunk_compress_blocks(uint32_t state[5], const void* blocks, size_t nblocks) {
+    if (!state || (nblocks && !blocks)) return fail(SHA1CHUNK_EINVAL, "null pointer");
+    if (nblocks == 0) return SHA1CHUNK_OK;
+    if (nblocks * 64 > 0xffffffffull) return fail(SHA1CHUNK_EINVAL, "too many blocks");
+    Device* D;
+    int rc = get_device(&D);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(D->mu);
+    const size_t bytes = nblocks * 64;
+    if ((rc = D->small.ensure(64 + bytes)) || (rc = D->small_pin.ensure(64 + bytes))) return rc;
+    uint8_t* h = static_cast<uint8_t*>(D->small_pin.p);
+    memcpy(h, state, 20);
+    memcpy(h + 64, blocks, bytes);
+    hipStream_t st = D->slot[0].stream;
+    HIP_TRY(hipMemcpyAsync(D->small.p, h, 64 + bytes, hipMemcpyHostToDevice, st));
+    uint8_t* d = static_cast<uint8_t*>(D->small.p);
+    BatchArgs A{};
+    A.base = d + 64;
+    A.ulen = static_cast<uint32_t>(bytes);
+    A.n = 1;
+    A.init_state = reinterpret_cast<const uint32_t*>(d);
+    A.out_state = reinterpret_cast<uint32_t*>(d + 32);
+    if ((rc = launch_checked(SHA1CHUNK_KERNEL_LANE, A, st))) return rc;
+    HIP_TRY(hipMemcpyAsync(h + 32, d + 32, 20, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    memcpy(state, h + 32, 20);
+    return SHA1CHUNK_OK;
+}
+
+int sha1chunk_finish(const uint32_t state[5], uint64_t prefix_bytes, const void* tail,
+                     uint32_t tail_len, uint8_t digest[20]) {
+    if (!state || !digest || (tail_len && !tail) || tail_len >= 64)
+        return fail(SHA1CHUNK_EINVAL, "bad argument");
+    Device* D;
+    int rc = get_device(&D);
+    if (rc) return rc;
+    std::lock_guard<std::mutex> lk(D->mu);
+    if ((rc = D->small.ensure(256)) || (rc = D->small_pin.ensure(256))) return rc;
+    uint8_t* h = static_cast<uint8_t*>(D->small_pin.p);
+    memcpy(h, state, 20);
+    if (tail_len) memcpy(h + 64, tail, tail_len);
+    hipStream_t st = D->slot[0].stream;
+    HIP_TRY(hipMemcpyAsync(D->small.p, h, 128, hipMemcpyHostToDevice, st));
+    uint8_t* d = static_cast<uint8_t*>(D->small.p);
+    BatchArgs A{};
+    A.base = d + 64;
+    A.ulen = tail_len;
+    A.n = 1;
+    A.init_state = reinterpret_cast<const uint32_t*>(d);
+    A.prefix_bytes = prefix_bytes;
+    A.dig = d + 128;
+    if ((rc = launch_checked(SHA1CHUNK_KERNEL_LANE, A, st))) return rc;
+    HIP_TRY(hipMemcpyAsync(h + 128, d + 128, 20, hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+    memcpy(digest, h + 128, 20);
+    return SHA1CHUNK_OK;
+}
+
+int sha1chunk_synth_fill_async(void* d_dst, uint64_t first, uint64_t count, uint32_t chunk_len,
+                               uint64_t seed, void* stream) {
+    if (count && !d_dst) return fail(SHA1CHUNK_EINVAL, "null pointer");
+    if ((reinterpret_cast<uintptr_t>(d_dst) & 7u) || (chunk_len & 7u && count > 1))
+        return fail(SHA1CHUNK_EALIGN, "synthetic chunks must start 8-byte aligned");
+    Device* D;
+    int rc = get_device(&D);
+    if (rc) return rc;
+    hipError_t e = launch_synth(static_cast<uint8_t*>(d_dst), nullptr, nullptr, chunk_len, first,
+                                count, seed, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "synth launch: %s", hipGetErrorString(e));
+    return SHA1CHUNK_OK;
+}
+
+int sha1chunk_synth_fill_ragged_async(void* d_base, const uint64_t* d_offsets,
+                                      const uint32_t* d_lengths, uint64_t first, uint64_t count,
+                                      uint64_t seed, void* stream) {
+    if (count && (!d_base || !d_offsets || !d_lengths)) return fail(SHA1CHUNK_EINVAL, "null pointer");
+    Device* D;
+    int rc = get_device(&D);
+    if (rc) return rc;
+    hipError_t e = launch_synth(static_cast<uint8_t*>(d_base), d_offsets, d_lengths, 0, first,
+                                count, seed, static_cast<hipStream_t>(stream));
+    if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "synth launch: %s", hipGetErrorString(e));
+    return SHA1CHUNK_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,321 @@
+"""Python view of libsha1chunk.so -- the MI355X SHA-1 chunk engine.
+
+Mirrors the reference's C hashing interface (same names, argument meaning and
+error behaviour; file:line into /root/reference):
+
+    shahash(data)                   chunk.c:35-51    one-shot SHA-1 -> 20 bytes
+    binary2hex / hex2binary         chunk.c:57-85    lowercase hex codec
+    make_chunks(path | file)        chunk.c:15-27    512 KiB chunk digests of a file
+    get_chunk_hash(chunk)           chunk.c:168-185  hex digest (prints 2 lines)
+    verify_hash(hex, data)          job.c:217-228    0 = match, 1 = mismatch
+    verify_chunk_hash(path, hex, i) chunk.c:204-217  exit(-1) on mismatch
+    SHA1()  .init/.update/.final    sha.h:58-60      streaming context
+
+plus the batch / device entry points of include/sha1chunk.h that replace a
+loop of shahash() calls.  Every digest is computed by the gfx950 HIP kernels;
+there is no CPU path.  The library must have been built (`make -C
+congestion-control-with-bittorren_amd` or __graft_entry__.build()); a missing
+library or device raises, it never falls back.
+
+PyTorch is only used for device memory and streams in the *_device helpers.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Iterable, Sequence
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libsha1chunk.so")
+CHUNK_LEN = 524288  # constants.h:14
+DIGEST_LEN = 20
+SEED = 0x5EED0001
+
+OK, EINVAL, ENODEV, ENOMEM, EHIP, EALIGN, EIO = 0, -1, -2, -3, -4, -5, -6
+HOST, DEVICE, ALL_DEVICES = 0, 1, 2
+KERNEL_AUTO, KERNEL_LANE, KERNEL_FUSED, KERNEL_SPLIT = 0, 1, 2, 3
+KERNELS = {"auto": KERNEL_AUTO, "lane": KERNEL_LANE, "fused": KERNEL_FUSED, "split": KERNEL_SPLIT}
+
+
+class Sha1ChunkError(RuntimeError):
+    def __init__(self, code: int, where: str, msg: str):
+        super().__init__(f"{where} failed ({code}): {msg}")
+        self.code = code
+
+
+class SHA1Context(C.Structure):
+    """Same 96-byte layout as the reference SHA1Context (sha.h:39-52)."""
+    _fields_ = [
+        ("totalLength", C.c_uint64),
+        ("hash", C.c_uint32 * 5),
+        ("bufferLength", C.c_uint32),
+        ("buffer", C.c_uint8 * 64),
+    ]
+
+
+_u8p = C.POINTER(C.c_uint8)
+_u32p = C.POINTER(C.c_uint32)
+_u64p = C.POINTER(C.c_uint64)
+_vp = C.c_void_p
+READER_FN = C.CFUNCTYPE(C.c_size_t, C.c_void_p, C.c_void_p, C.c_size_t)
+SINK_FN = C.CFUNCTYPE(None, C.c_void_p, C.c_size_t, _u8p, C.c_size_t)
+
+# (name, restype, argtypes) of every symbol the C ABI exports.
+_SIGNATURES = [
+    ("SHA1Init", None, [C.POINTER(SHA1Context)]),
+    ("SHA1Update", None, [C.POINTER(SHA1Context), _vp, C.c_uint32]),
+    ("SHA1Final", None, [C.POINTER(SHA1Context), _u8p]),
+    ("shahash", None, [_u8p, C.c_int, _u8p]),
+    ("binary2hex", None, [_u8p, C.c_int, C.c_char_p]),
+    ("hex2binary", None, [C.c_char_p, C.c_int, _u8p]),
+    ("make_chunks", C.c_int, [_vp, C.POINTER(_u8p)]),
+    ("get_chunk_hash", C.c_void_p, [C.c_char_p, C.c_size_t]),
+    ("verify_chunk_hash", None, [_vp, C.c_char_p, C.c_size_t]),
+    ("verify_hash", C.c_int, [C.c_char_p, C.c_char_p]),
+    ("sha1chunk_hash_batch", C.c_int, [_vp, _u64p, _u32p, C.c_size_t, _u8p, C.c_uint]),
+    ("sha1chunk_verify_batch", C.c_int, [_vp, _u64p, _u32p, C.c_size_t, _u8p, _u8p, C.c_uint]),
+    ("sha1chunk_hash_device_async", C.c_int, [_vp, _vp, _vp, C.c_size_t, _vp, _vp, C.c_int]),
+    ("sha1chunk_hash_uniform_async", C.c_int, [_vp, C.c_uint32, C.c_size_t, _vp, _vp, C.c_int]),
+    ("sha1chunk_compare_device_async", C.c_int, [_vp, _vp, C.c_size_t, _vp, _vp]),
+    ("sha1chunk_hash_stream", C.c_long, [READER_FN, _vp, SINK_FN, _vp]),
+    ("sha1chunk_hash_fd", C.c_long, [C.c_int, _u8p, C.c_size_t, C.POINTER(C.c_size_t)]),
+    ("sha1chunk_compress_blocks", C.c_int, [_u32p, _vp, C.c_size_t]),
+    ("sha1chunk_finish", C.c_int, [_u32p, C.c_uint64, _vp, C.c_uint32, _u8p]),
+    ("sha1chunk_synth_fill_async", C.c_int, [_vp, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, _vp]),
+    ("sha1chunk_synth_fill_ragged_async", C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64, _vp]),
+    ("sha1chunk_device_count", C.c_int, []),
+    ("sha1chunk_set_device", C.c_int, [C.c_int]),
+    ("sha1chunk_get_device", C.c_int, []),
+    ("sha1chunk_last_error", C.c_char_p, []),
+    ("sha1chunk_version", C.c_char_p, []),
+]
+
+_lib: C.CDLL | None = None
+
+
+def lib() -> C.CDLL:
+    """Load libsha1chunk.so (raises if it was never built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise FileNotFoundError(
+                f"{LIB_PATH} is missing: build it with __graft_entry__.build() or "
+                "`make -C congestion-control-with-bittorren_amd`")
+        L = C.CDLL(LIB_PATH)
+        for name, res, args in _SIGNATURES:
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        L.free = C.CDLL(None).free
+        L.free.argtypes = [C.c_void_p]
+        _lib = L
+    return _lib
+
+
+def exported_symbols() -> list[str]:
+    return [s[0] for s in _SIGNATURES]
+
+
+def _check(rc: int, where: str) -> int:
+    if rc < 0:
+        raise Sha1ChunkError(rc, where, lib().sha1chunk_last_error().decode(errors="replace"))
+    return rc
+
+
+def _np_ptr(a: np.ndarray, t=_u8p):
+    return a.ctypes.data_as(t)
+
+
+# ------------------------------------------------------------ device mgmt --
+def device_count() -> int:
+    n = lib().sha1chunk_device_count()
+    return max(n, 0)
+
+
+def set_device(dev: int) -> None:
+    _check(lib().sha1chunk_set_device(dev), "sha1chunk_set_device")
+
+
+def version() -> str:
+    return lib().sha1chunk_version().decode()
+
+
+# ------------------------------------------------- reference-named API ----
+def binary2hex(buf: bytes) -> str:
+    """chunk.c:57-63 -- lowercase hex of buf."""
+    b = np.frombuffer(bytes(buf) + b"\0", np.uint8)
+    out = C.create_string_buffer(2 * len(buf) + 1)
+    lib().binary2hex(_np_ptr(b), len(buf), out)
+    return out.value.decode()
+
+
+def hex2binary(hexstr: str) -> bytes:
+    """chunk.c:78-85 -- hex (either case) to bytes."""
+    raw = hexstr.encode()
+    out = np.zeros(max(len(raw) // 2, 1), np.uint8)
+    lib().hex2binary(raw, len(raw), _np_ptr(out))
+    return out[: len(raw) // 2].tobytes()
+
+
+def shahash(data: bytes | np.ndarray) -> bytes:
+    """chunk.c:35-51 -- SHA-1 of data on the device."""
+    buf = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else \
+        np.ascontiguousarray(data, np.uint8).reshape(-1)
+    n = buf.size
+    if n == 0:
+        buf = np.zeros(1, np.uint8)
+    out = np.zeros(DIGEST_LEN, np.uint8)
+    off = np.zeros(1, np.uint64)
+    ln = np.array([n], np.uint32)
+    _check(lib().sha1chunk_hash_batch(buf.ctypes.data, _np_ptr(off, _u64p), _np_ptr(ln, _u32p), 1,
+                                      _np_ptr(out), HOST), "shahash")
+    return out.tobytes()
+
+
+def get_chunk_hash(chunk: bytes) -> str:
+    """chunk.c:168-185 -- hex digest; the C side prints the reference's two lines."""
+    p = lib().get_chunk_hash(bytes(chunk), len(chunk))
+    try:
+        return C.string_at(p).decode()
+    finally:
+        lib().free(p)
+
+
+def verify_hash(chunk_hash: str, data: bytes) -> int:
+    """job.c:217-228 -- hashes CHUNK_LEN bytes of data; 0 = match, 1 = mismatch."""
+    buf = bytes(data)
+    if len(buf) < CHUNK_LEN:
+        raise ValueError("verify_hash reads CHUNK_LEN (524288) bytes of data")
+    return lib().verify_hash(chunk_hash.encode(), buf)
+
+
+def make_chunks(src) -> list[bytes]:
+    """chunk.c:15-27 -- digests of every 512 KiB chunk of a file (path or
+    binary file object opened on a real fd)."""
+    if isinstance(src, (str, os.PathLike)):
+        with open(src, "rb") as f:
+            return make_chunks(f)
+    fd = src.fileno()
+    pos = src.tell()
+    os.lseek(fd, pos, os.SEEK_SET)
+    size = os.fstat(fd).st_size - pos
+    cap = max((size + CHUNK_LEN - 1) // CHUNK_LEN, 1)
+    out = np.zeros((cap, DIGEST_LEN), np.uint8)
+    total = C.c_size_t(0)
+    n = _check(lib().sha1chunk_hash_fd(fd, _np_ptr(out), cap, C.byref(total)), "make_chunks")
+    if total.value > cap:
+        raise Sha1ChunkError(EIO, "make_chunks", "file grew while hashing")
+    return [out[i].tobytes() for i in range(n)]
+
+
+class SHA1:
+    """sha.h:58-60 streaming context (SHA1Init / SHA1Update / SHA1Final)."""
+
+    def __init__(self):
+        self.ctx = SHA1Context()
+        lib().SHA1Init(C.byref(self.ctx))
+
+    def update(self, data: bytes) -> "SHA1":
+        b = bytes(data)
+        lib().SHA1Update(C.byref(self.ctx), b, len(b))
+        return self
+
+    def final(self) -> bytes:
+        out = np.zeros(DIGEST_LEN, np.uint8)
+        lib().SHA1Final(C.byref(self.ctx), _np_ptr(out))
+        return out.tobytes()
+
+
+# ------------------------------------------------------------- batch API --
+def hash_batch(base: np.ndarray | bytes, offsets: Sequence[int], lengths: Sequence[int],
+               all_devices: bool = False) -> np.ndarray:
+    """digests[i] = SHA-1(base[offsets[i]:offsets[i]+lengths[i]]) -> (n, 20) uint8."""
+    b = np.frombuffer(base, np.uint8) if isinstance(base, (bytes, bytearray)) else \
+        np.ascontiguousarray(base).view(np.uint8).reshape(-1)
+    if b.size == 0:
+        b = np.zeros(1, np.uint8)
+    off = np.ascontiguousarray(offsets, np.uint64)
+    ln = np.ascontiguousarray(lengths, np.uint32)
+    if off.shape != ln.shape:
+        raise ValueError("offsets and lengths differ in length")
+    if off.size and int((off + ln).max()) > (b.size if len(base) else 0):
+        raise ValueError("chunk range outside the buffer")
+    out = np.zeros((off.size, DIGEST_LEN), np.uint8)
+    flags = ALL_DEVICES if all_devices else HOST
+    _check(lib().sha1chunk_hash_batch(b.ctypes.data, _np_ptr(off, _u64p), _np_ptr(ln, _u32p),
+                                      off.size, _np_ptr(out), flags), "sha1chunk_hash_batch")
+    return out
+
+
+def verify_batch(base, offsets, lengths, expected: np.ndarray) -> np.ndarray:
+    """verify_hash() semantics per chunk: 0 = match, 1 = mismatch."""
+    b = np.ascontiguousarray(np.frombuffer(base, np.uint8) if isinstance(base, (bytes, bytearray))
+                             else base).view(np.uint8).reshape(-1)
+    off = np.ascontiguousarray(offsets, np.uint64)
+    ln = np.ascontiguousarray(lengths, np.uint32)
+    exp = np.ascontiguousarray(expected, np.uint8).reshape(-1, DIGEST_LEN)
+    mism = np.zeros(off.size, np.uint8)
+    _check(lib().sha1chunk_verify_batch(b.ctypes.data, _np_ptr(off, _u64p), _np_ptr(ln, _u32p),
+                                        off.size, _np_ptr(exp), _np_ptr(mism), HOST),
+           "sha1chunk_verify_batch")
+    return mism
+
+
+# ------------------------------------------------------ device (torch) ----
+def _stream_ptr(stream) -> int | None:
+    if stream is None:
+        import torch
+        return torch.cuda.current_stream().cuda_stream
+    return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+
+def hash_device(base, offsets, lengths, digests, stream=None, kernel: int | str = KERNEL_AUTO) -> None:
+    """Enqueue the hash of a device-resident batch (torch CUDA tensors:
+    base uint8, offsets int64, lengths int32, digests uint8 (n, 20))."""
+    k = KERNELS[kernel] if isinstance(kernel, str) else kernel
+    n = offsets.numel()
+    _check(lib().sha1chunk_hash_device_async(base.data_ptr(), offsets.data_ptr(), lengths.data_ptr(),
+                                             n, digests.data_ptr(), _stream_ptr(stream), k),
+           "sha1chunk_hash_device_async")
+
+
+def hash_uniform_device(base, chunk_len: int, n: int, digests, stream=None,
+                        kernel: int | str = KERNEL_AUTO) -> None:
+    k = KERNELS[kernel] if isinstance(kernel, str) else kernel
+    _check(lib().sha1chunk_hash_uniform_async(base.data_ptr(), chunk_len, n, digests.data_ptr(),
+                                              _stream_ptr(stream), k),
+           "sha1chunk_hash_uniform_async")
+
+
+def compare_device(digests, expected, mismatch, stream=None) -> None:
+    _check(lib().sha1chunk_compare_device_async(digests.data_ptr(), expected.data_ptr(),
+                                                mismatch.numel(), mismatch.data_ptr(),
+                                                _stream_ptr(stream)),
+           "sha1chunk_compare_device_async")
+
+
+def synth_fill_device(dst, first: int, count: int, chunk_len: int = CHUNK_LEN, seed: int = SEED,
+                      stream=None) -> None:
+    _check(lib().sha1chunk_synth_fill_async(dst.data_ptr(), first, count, chunk_len, seed,
+                                            _stream_ptr(stream)), "sha1chunk_synth_fill_async")
+
+
+def synth_fill_ragged_device(base, offsets, lengths, first: int, seed: int = SEED,
+                             stream=None) -> None:
+    _check(lib().sha1chunk_synth_fill_ragged_async(base.data_ptr(), offsets.data_ptr(),
+                                                   lengths.data_ptr(), first, offsets.numel(),
+                                                   seed, _stream_ptr(stream)),
+           "sha1chunk_synth_fill_ragged_async")
+
+
+def ragged_layout(lengths: Iterable[int], align: int = 128) -> tuple[np.ndarray, int]:
+    """Offsets packing chunks back to back at `align`-byte boundaries."""
+    ln = np.asarray(list(lengths) if not isinstance(lengths, np.ndarray) else lengths, np.uint64)
+    padded = (ln + (align - 1)) // align * align
+    off = np.zeros(ln.size, np.uint64)
+    if ln.size > 1:
+        off[1:] = np.cumsum(padded)[:-1]
+    total = int(padded.sum()) if ln.size else 0
+    return off, total

@@ -1,0 +1,126 @@
+/*
+ * sha1chunk.h -- the batch entry points of the MI355X SHA-1 chunk engine
+ * (libsha1chunk.so).  Plain C ABI: pointers, sizes, a `void *` HIP stream.
+ *
+ * These are the one new interface SURVEY.md 7.1 step 2 asks for.  The
+ * reference has no batch API: every digest in /root/reference is produced by
+ * a serial shahash() call (chunk.c:23 from make_chunks, chunk.c:180 from
+ * get_chunk_hash <- job.c:218 verify_hash and chunk.c:208 verify_chunk_hash).
+ * sha1chunk_hash_batch() replaces a loop of those calls; the reference-
+ * signature functions in chunk_hash.h / sha.h are implemented on top of it.
+ *
+ * Error convention: 0 on success, a negative SHA1CHUNK_E* code otherwise
+ * (never exit()); sha1chunk_last_error() returns a thread-local message.
+ * There is no CPU hashing path: without a usable gfx950 device every call
+ * fails with SHA1CHUNK_ENODEV.
+ */
+#ifndef SHA1CHUNK_H
+#define SHA1CHUNK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SHA1CHUNK_DIGEST_LEN 20
+#define SHA1CHUNK_CHUNK_LEN 524288 /* constants.h:14 CHUNK_LEN */
+
+enum {
+    SHA1CHUNK_OK = 0,
+    SHA1CHUNK_EINVAL = -1, /* bad argument                                   */
+    SHA1CHUNK_ENODEV = -2, /* no HIP device / runtime                        */
+    SHA1CHUNK_ENOMEM = -3, /* device or pinned allocation failed             */
+    SHA1CHUNK_EHIP = -4,   /* HIP runtime error (see sha1chunk_last_error)   */
+    SHA1CHUNK_EALIGN = -5, /* digest (4 B) / synthetic (8 B) buffer misaligned */
+    SHA1CHUNK_EIO = -6     /* read error on a file descriptor                */
+};
+
+/* Where the buffers of sha1chunk_hash_batch / sha1chunk_verify_batch live. */
+#define SHA1CHUNK_HOST 0u        /* host memory: staged through pinned buffers  */
+#define SHA1CHUNK_DEVICE 1u      /* device memory of the current device         */
+#define SHA1CHUNK_ALL_DEVICES 2u /* HOST only: shard the chunk list over every
+                                    visible device, one host thread per device */
+
+/* Kernel choice for the device entry points (AUTO picks by batch shape). */
+enum {
+    SHA1CHUNK_KERNEL_AUTO = 0,
+    SHA1CHUNK_KERNEL_LANE = 1,  /* one lane per chunk, per-lane loads; any alignment */
+    SHA1CHUNK_KERNEL_FUSED = 2, /* one lane per chunk, LDS-staged coalesced loads    */
+    SHA1CHUNK_KERNEL_SPLIT = 3  /* schedule-producer + round-consumer wave pairs      */
+};
+
+/* digests[i*20 .. i*20+19] = SHA-1(base[offsets[i] .. offsets[i]+lengths[i])).
+ * Synchronous.  Host mode accepts any alignment and overlapping chunks. */
+int sha1chunk_hash_batch(const void *base, const uint64_t *offsets, const uint32_t *lengths,
+                         size_t n, uint8_t *digests, unsigned flags);
+
+/* mismatch[i] = 0 if the digest of chunk i equals expected[i*20..], else 1
+ * (the verify_hash() convention of job.c:217-228). */
+int sha1chunk_verify_batch(const void *base, const uint64_t *offsets, const uint32_t *lengths,
+                           size_t n, const uint8_t *expected, uint8_t *mismatch, unsigned flags);
+
+/* Device-resident, asynchronous on `stream` (a hipStream_t, NULL = default).
+ * All pointers are device pointers.  Returns after enqueueing. */
+int sha1chunk_hash_device_async(const void *d_base, const uint64_t *d_offsets,
+                                const uint32_t *d_lengths, size_t n, uint8_t *d_digests,
+                                void *stream, int kernel);
+
+/* Same for n equal chunks of chunk_len bytes laid back to back at d_base
+ * (the make_chunks layout): no offset/length arrays needed. */
+int sha1chunk_hash_uniform_async(const void *d_base, uint32_t chunk_len, size_t n,
+                                 uint8_t *d_digests, void *stream, int kernel);
+
+/* Device compare of computed vs expected digests -> mismatch bytes. */
+int sha1chunk_compare_device_async(const uint8_t *d_digests, const uint8_t *d_expected,
+                                   size_t n, uint8_t *d_mismatch, void *stream);
+
+/* Hash a byte stream in 512 KiB chunks (the last one at its true length,
+ * as make_chunks does, chunk.c:22-23) through a pinned double-buffered
+ * read -> H2D -> hash -> D2H pipeline.  `reader` fills up to n bytes of dst
+ * (pinned memory) and returns the count, 0 at end of stream, or (size_t)-1
+ * on error; `sink` receives each completed run of digests in order.
+ * Returns the number of chunks (>= 0) or a negative error. */
+typedef size_t (*sha1chunk_reader_fn)(void *ctx, void *dst, size_t n);
+typedef void (*sha1chunk_sink_fn)(void *ctx, size_t first_chunk, const uint8_t *digests,
+                                  size_t count);
+long sha1chunk_hash_stream(sha1chunk_reader_fn reader, void *reader_ctx, sha1chunk_sink_fn sink,
+                           void *sink_ctx);
+/* File-descriptor convenience: up to max_chunks digests into `digests`;
+ * *total_chunks (optional) gets the file's chunk count. */
+long sha1chunk_hash_fd(int fd, uint8_t *digests, size_t max_chunks, size_t *total_chunks);
+
+/* Streaming support for SHA1Update/SHA1Final: compress nblocks whole 64-byte
+ * blocks (host memory) into the chaining value state[5]. */
+int sha1chunk_compress_blocks(uint32_t state[5], const void *blocks, size_t nblocks);
+/* Finish a stream: state[5] after prefix_bytes hashed bytes, then tail_len
+ * (< 64) buffered bytes -> padded final block(s) -> 20-byte digest. */
+int sha1chunk_finish(const uint32_t state[5], uint64_t prefix_bytes, const void *tail,
+                     uint32_t tail_len, uint8_t digest[20]);
+
+/* Synthetic corpus generated on the device: chunk c, 64-bit
+ * LE word w = splitmix64(seed ^ (c << 24) ^ w), chunks first..first+count-1
+ * written back to back, chunk_len bytes each. */
+int sha1chunk_synth_fill_async(void *d_dst, uint64_t first, uint64_t count, uint32_t chunk_len,
+                               uint64_t seed, void *stream);
+/* Ragged variant: chunk first+i of d_lengths[i] bytes at d_base + d_offsets[i]
+ * (device arrays; every d_base + d_offsets[i] 8-byte aligned). */
+int sha1chunk_synth_fill_ragged_async(void *d_base, const uint64_t *d_offsets,
+                                      const uint32_t *d_lengths, uint64_t first, uint64_t count,
+                                      uint64_t seed, void *stream);
+
+/* Device management. */
+int sha1chunk_device_count(void);
+int sha1chunk_set_device(int device);
+int sha1chunk_get_device(void);
+/* Last error text of this thread ("" if none). */
+const char *sha1chunk_last_error(void);
+/* "gfx950:<kernels>" build identity, for logs. */
+const char *sha1chunk_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

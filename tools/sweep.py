@@ -1,0 +1,69 @@
+#!/usr/bin/env python3
+"""Kernel sweep on one GPU: GiB/s of each hashing kernel vs chunk count, all
+kernels interleaved in one process (cdna_hip_programming.md rule 24), on the
+same device-resident synthetic chunks.  Prints one JSON line per point and a
+summary table; used to tune choose_kernel() in sha1_runtime.hip."""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--chunks", default="1024,4096,16384,65536")
+    ap.add_argument("--chunk-len", type=int, default=524288)
+    ap.add_argument("--kernels", default="lane,fused,split")
+    ap.add_argument("--rounds", type=int, default=3)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    import torch
+    pkg = importlib.import_module("congestion-control-with-bittorren_amd")
+    torch.cuda.set_device(0)
+    pkg.set_device(0)
+    L = a.chunk_len
+    kernels = a.kernels.split(",")
+    rows = []
+    for n in [int(x) for x in a.chunks.split(",")]:
+        buf = torch.empty(n * L, dtype=torch.uint8, device="cuda")
+        pkg.synth_fill_device(buf, 0, n, L)
+        ref = None
+        times = {k: [] for k in kernels}
+        for _ in range(a.rounds):
+            for k in kernels:
+                dig = torch.zeros((n, 20), dtype=torch.uint8, device="cuda")
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                pkg.hash_uniform_device(buf, L, n, dig, kernel=k)
+                e1.record()
+                torch.cuda.synchronize()
+                times[k].append(e0.elapsed_time(e1))
+                d = dig.cpu().numpy()
+                if ref is None:
+                    ref = d
+                assert np.array_equal(d, ref), f"kernel {k} disagrees at n={n}"
+        for k in kernels:
+            ms = float(np.median(times[k]))
+            row = {"chunks": n, "chunk_bytes": L, "kernel": k, "ms": round(ms, 4),
+                   "GiBps": round(n * L / (ms * 1e-3) / 2**30, 2),
+                   "hbm_frac": round(n * (L + 20) / (ms * 1e-3) / 8e12, 5),
+                   "all_ms": [round(t, 4) for t in times[k]]}
+            rows.append(row)
+            print(json.dumps(row), flush=True)
+        del buf
+        torch.cuda.empty_cache()
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(rows, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
