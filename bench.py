@@ -125,7 +125,7 @@ def main():
     alg_bytes = n * (L + 20)  # per launch: every chunk byte read once + its digest
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     blocks = n * ((L + 8) // 64 + 1)
-    valu_tops = blocks * 64 * VALU_OPS_PER_BLOCK / (kern_ms * 1e-3) / 1e12
+    valu_tops = blocks * VALU_OPS_PER_BLOCK / (kern_ms * 1e-3) / 1e12
 
     result = {
         "metric": METRIC,

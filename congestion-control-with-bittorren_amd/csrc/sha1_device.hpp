@@ -61,7 +61,15 @@ __device__ __forceinline__ void round_step(uint32_t (&v)[5], uint32_t wt) {
         f = xor3(v[ib], v[ic], v[id]);
         k = K3;
     }
-    v[ie] = v[ie] + rotl(v[ia], 5) + f + k + wt;
+    // temp = ROTL5(a) + F + e + K + W.  e + K + W does not depend on a, so it
+    // is summed first, off the chain; the chain a -> {ROTL5(a), F} -> add3
+    // is then 2 dependent VALU ops per round instead of 3.  The add3 is
+    // pinned in asm because LLVM otherwise re-associates the 5-term sum as
+    // (e + ROTL5(a) + F) + (W + K), putting both adds on the chain.
+    const uint32_t x = v[ie] + wt + k;
+    uint32_t t;
+    asm("v_add3_u32 %0, %1, %2, %3" : "=v"(t) : "v"(rotl(v[ia], 5)), "v"(f), "v"(x));
+    v[ie] = t;
     v[ib] = rotl(v[ib], 30);
 }
 
@@ -101,16 +109,14 @@ __device__ __forceinline__ void compress(uint32_t (&h)[5], uint32_t (&w)[16]) {
 
 // Rounds only, with the 80-word schedule supplied in registers (split
 // kernel consumer: the producer wave computed it).
-template <int T>
+template <int T, int END = 80>
 struct RoundsW {
     __device__ __forceinline__ static void run(uint32_t (&v)[5], const uint32_t (&W)[80]) {
-        round_step<T>(v, W[T]);
-        RoundsW<T + 1>::run(v, W);
+        if constexpr (T < END) {
+            round_step<T>(v, W[T]);
+            RoundsW<T + 1, END>::run(v, W);
+        }
     }
-};
-template <>
-struct RoundsW<80> {
-    __device__ __forceinline__ static void run(uint32_t (&)[5], const uint32_t (&)[80]) {}
 };
 
 // Padding of the final partial block (sha.c:536-543): word i of the block
@@ -139,28 +145,31 @@ __device__ __forceinline__ void init_state(uint32_t (&h)[5]) {
 // message byte, so they never cross into an unmapped page.  Output: the
 // block's words as LITTLE-endian loads (byte-swap is done by the caller).
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void load_block_full(const uint8_t* p, uint32_t (&w)[16]) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    if ((a & 15u) == 0) {
-        const uint4* q = reinterpret_cast<const uint4*>(p);
+// 16-byte-aligned block: 4 x global_load_dwordx4, no branches (so hipcc can
+// count the loads with a partial vmcnt when they are prefetched).
+__device__ __forceinline__ void load_block_a16(const uint8_t* p, uint32_t (&w)[16]) {
+    const uint4* q = reinterpret_cast<const uint4*>(p);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint4 x = q[j];
-            w[4 * j + 0] = x.x;
-            w[4 * j + 1] = x.y;
-            w[4 * j + 2] = x.z;
-            w[4 * j + 3] = x.w;
-        }
-    } else {
-        const uint32_t sh = static_cast<uint32_t>(a & 3u);
-        const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
-        uint32_t d[17];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) d[j] = q[j];
-        d[16] = sh ? q[16] : 0u;
-#pragma unroll
-        for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
+    for (int j = 0; j < 4; ++j) {
+        const uint4 x = q[j];
+        w[4 * j + 0] = x.x;
+        w[4 * j + 1] = x.y;
+        w[4 * j + 2] = x.z;
+        w[4 * j + 3] = x.w;
     }
+}
+
+// Any alignment: 16 (+1) aligned dword loads and v_alignbyte funnel shifts.
+__device__ __forceinline__ void load_block_any(const uint8_t* p, uint32_t (&w)[16]) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t sh = static_cast<uint32_t>(a & 3u);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+    uint32_t d[17];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) d[j] = q[j];
+    d[16] = sh ? q[16] : 0u;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
 }
 
 __device__ __forceinline__ void load_block_partial(const uint8_t* p, uint32_t avail,

@@ -23,7 +23,8 @@ struct BatchArgs {
 
 hipError_t launch_lane(const BatchArgs& A, hipStream_t st);
 hipError_t launch_fused(const BatchArgs& A, hipStream_t st);
-hipError_t launch_split(const BatchArgs& A, hipStream_t st);
+// unit_blocks (1..3): schedule blocks per producer/consumer barrier; LDS = unit_blocks * 40 KiB
+hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st);
 hipError_t launch_synth(uint8_t* dst, const uint64_t* off, const uint32_t* lens, uint32_t ulen,
                         uint64_t first, uint64_t count, uint64_t seed, hipStream_t st);
 hipError_t launch_compare(const uint8_t* dig, const uint8_t* exp, uint32_t n, uint8_t* mismatch,

@@ -67,14 +67,22 @@ __device__ __forceinline__ void emit(const BatchArgs& A, uint32_t id, const uint
 }
 
 // Blocks [k0, nfull) of one lane straight from global memory, then the
-// padded tail (unless the batch is in update mode).
-__device__ __forceinline__ void lane_blocks(const BatchArgs& A, const Entry& en, uint32_t k0,
-                                            uint32_t (&h)[5]) {
+// padded tail (unless the batch is in update mode).  A16 selects the
+// branch-free 16-byte-aligned loader (chosen per wave), so the one-block
+// register prefetch is counted with a partial vmcnt.
+template <bool A16>
+__device__ __forceinline__ void lane_loop(const Entry& en, uint32_t k0, uint32_t (&h)[5]) {
     const uint32_t nfull = en.len >> 6;
     uint32_t cur[16], nxt[16];
-    if (k0 < nfull) load_block_full(en.p + 64ull * k0, cur);
+    if (k0 < nfull) {
+        if constexpr (A16) load_block_a16(en.p + 64ull * k0, cur);
+        else load_block_any(en.p + 64ull * k0, cur);
+    }
     for (uint32_t k = k0; k < nfull; ++k) {
-        if (k + 1 < nfull) load_block_full(en.p + 64ull * (k + 1), nxt);
+        if (k + 1 < nfull) {
+            if constexpr (A16) load_block_a16(en.p + 64ull * (k + 1), nxt);
+            else load_block_any(en.p + 64ull * (k + 1), nxt);
+        }
         uint32_t w[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) w[j] = bswap(cur[j]);
@@ -82,6 +90,18 @@ __device__ __forceinline__ void lane_blocks(const BatchArgs& A, const Entry& en,
 #pragma unroll
         for (int j = 0; j < 16; ++j) cur[j] = nxt[j];
     }
+}
+
+__device__ __forceinline__ bool wave_all(bool x) { return __ballot(!x) == 0; }
+
+__device__ __forceinline__ void lane_blocks(const BatchArgs& A, const Entry& en, uint32_t k0,
+                                            uint32_t (&h)[5]) {
+    const bool a16 = (reinterpret_cast<uintptr_t>(en.p) & 15u) == 0;
+    if (wave_all(a16))
+        lane_loop<true>(en, k0, h);
+    else
+        lane_loop<false>(en, k0, h);
+    const uint32_t nfull = en.len >> 6;
     if (!A.out_state)
         finish_message(h, en.p + 64ull * nfull, en.len & 63u, A.prefix_bytes + en.len);
 }
@@ -292,33 +312,52 @@ __global__ __launch_bounds__(64) void sha1_fused_kernel(BatchArgs A) {
 }
 
 // --------------------------------------------------------------- split ----
-// LDS: raw ring (producer only) + 2-slot W ring.  W slot layout: group q of
-// four schedule words (q = 0..19) of lane r at q*1024 + r*16, so both the
-// producer's ds_write_b128 and the consumer's ds_read_b128 touch one
-// contiguous KiB per instruction (conflict-free).
-constexpr int kSplitRaw = 3;
-constexpr int kWSlotBytes = 20 * 1024;
+// Workgroup = consumer wave (wave 0) + producer wave (wave 1) on the same 64
+// chunks.  The producer streams each lane's blocks from HBM (per-lane
+// 16-byte loads, two blocks in flight in registers), byte-swaps them and
+// expands the 80-word schedule into an LDS ring; the consumer runs only the
+// 80 rounds, so each chunk's serial instruction stream (the bound when
+// there are too few chunks to fill the SIMDs) drops from ~630 to ~440
+// instructions per block.
+//
+// The ring has 2 slots of U blocks (U*20 KiB each).  W slot layout: group q
+// (q = 0..19) of four schedule words of block j of lane r at
+// j*20K + q*1K + r*16, so every ds_write_b128 / ds_read_b128 touches one
+// contiguous KiB (conflict-free).  Protocol, one s_barrier per unit of U
+// blocks (each wave executes ceil(Tmax/U)+1 of them):
+//   producer: write unit m (blocks mU..mU+U-1) into slot m&1 -> B_m
+//   consumer: B_0, read W(0); per block k: [if k+1 starts unit m+1: B_{m+1}]
+//             stream W(k+1) into the spare register set, rounds of block k.
+//   RAW: unit m+1 is complete before B_{m+1}; its reads come after it.
+//   WAR: the producer rewrites slot m&1 (unit m+2) only after B_{m+1}; every
+//        read of unit m was issued before B_{m+1} and drained by its lgkmcnt(0).
+// Fewer barriers per block (U > 1) is worth ~10% at low occupancy; U = 1
+// keeps LDS at 40 KiB for higher occupancy.
+constexpr int kWBlockBytes = 20 * 1024;
 
+// The lgkmcnt(0) goes through the builtin so hipcc knows every LDS access
+// before the barrier has completed (it then stops waiting for them later);
+// the barrier itself is asm with a memory clobber so no LDS access moves
+// across it.
 __device__ __forceinline__ void split_barrier() {
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0) only (gfx9 encoding)
+    asm volatile("s_barrier" ::: "memory");
 }
 
-// Producer: fill the schedule of block k into W slot `slot`.
+// Producer: the 80-word schedule of one block into its W block slot.
 template <int T>
 struct SchedWrite {
     __device__ __forceinline__ static void run(uint32_t (&w)[16], uint8_t* slot, int lane) {
-        if constexpr (T >= 16) sched_step<T>(w);
-        if constexpr ((T & 3) == 3) {
-            constexpr int j = (T - 3) & 15;
-            *reinterpret_cast<uint4*>(slot + (T >> 2) * 1024 + lane * 16) =
-                make_uint4(w[j], w[j + 1], w[j + 2], w[j + 3]);
+        if constexpr (T < 80) {
+            if constexpr (T >= 16) sched_step<T>(w);
+            if constexpr ((T & 3) == 3) {
+                constexpr int j = (T - 3) & 15;
+                *reinterpret_cast<uint4*>(slot + (T >> 2) * 1024 + lane * 16) =
+                    make_uint4(w[j], w[j + 1], w[j + 2], w[j + 3]);
+            }
+            SchedWrite<T + 1>::run(w, slot, lane);
         }
-        SchedWrite<T + 1>::run(w, slot, lane);
     }
-};
-template <>
-struct SchedWrite<80> {
-    __device__ __forceinline__ static void run(uint32_t (&)[16], uint8_t*, int) {}
 };
 
 __device__ __forceinline__ uint32_t total_blocks(uint32_t len) {
@@ -326,97 +365,186 @@ __device__ __forceinline__ uint32_t total_blocks(uint32_t len) {
     return (len >> 6) + (((len & 63u) < 56u) ? 1u : 2u);
 }
 
+// Message words of block k for the producer's tail region (any block of any
+// lane: full, partial+pad, length-only), big-endian, padding applied.
+__device__ __forceinline__ void tail_block_words(const Entry& en, uint32_t k, uint32_t (&w)[16]) {
+    const uint32_t nfull = en.len >> 6, rem = en.len & 63u;
+    const uint64_t bits = (uint64_t)en.len * 8ull;
+    if (k < nfull) {
+        load_block_any(en.p + 64ull * k, w);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
+    } else if (k == nfull) {
+        if (rem) {
+            load_block_partial(en.p + 64ull * k, rem, w);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; ++j) w[j] = 0u;
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = pad_word(bswap(w[j]), j, (int)rem);
+        if (rem < 56u) {
+            w[14] = (uint32_t)(bits >> 32);
+            w[15] = (uint32_t)bits;
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 14; ++j) w[j] = 0u;
+        w[14] = (uint32_t)(bits >> 32);
+        w[15] = (uint32_t)bits;
+    }
+}
+
+template <int U>
+__device__ __forceinline__ void produce_block(uint32_t k, uint32_t (&w)[16], uint8_t* ring, int lane) {
+    const uint32_t m = k / U, j = k - m * U;
+    SchedWrite<0>::run(w, ring + ((m & 1u) * U + j) * kWBlockBytes, lane);
+    if (j == U - 1) split_barrier();
+}
+
+// Two blocks (128 contiguous bytes) of one lane's chunk, loaded per lane.
+struct Stage {
+    uint32_t w[32];
+};
+__device__ __forceinline__ void load_stage(const uint8_t* p, Stage& st) {
+    uint32_t a[16], b[16];
+    load_block_a16(p, a);
+    load_block_a16(p + 64, b);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        st.w[j] = a[j];
+        st.w[16 + j] = b[j];
+    }
+}
+
+// Producer side of one bulk stage: blocks 2s, 2s+1 from `cur`; once the
+// second block's words are taken, `cur` is refilled with stage s+2.
+template <int U>
+__device__ __forceinline__ void produce_stage(const Entry& en, uint32_t s, uint32_t S, Stage& cur,
+                                              uint8_t* ring, int lane) {
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        uint32_t w[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = bswap(cur.w[16 * half + j]);
+        if (half == 1 && s + 2 < S) load_stage(en.p + 128ull * (s + 2), cur);
+        produce_block<U>(2 * s + half, w, ring, lane);
+    }
+}
+
+template <int P>
+__device__ __forceinline__ void read_w_group(const uint8_t* slot, uint32_t (&W)[80]) {
+#pragma unroll
+    for (int q = 5 * P; q < 5 * P + 5; ++q) {
+        const uint4 x = *reinterpret_cast<const uint4*>(slot + q * 1024);
+        W[4 * q + 0] = x.x;
+        W[4 * q + 1] = x.y;
+        W[4 * q + 2] = x.z;
+        W[4 * q + 3] = x.w;
+    }
+}
+
+// Consumer: rounds of block k from Wc while W(k+1) streams into Wn.  All of
+// it is straight-line (the barrier position is a compile-time function of
+// the unrolled block index), so hipcc inserts no waits inside the rounds.
+template <int U, int J>
+__device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (&h)[5],
+                                              const uint32_t (&Wc)[80], uint32_t (&Wn)[80],
+                                              const uint8_t* ring, int lane) {
+    // block k+1 = unit m', sub-block j'; barrier when it opens a new unit
+    constexpr int jn = (J + 1) % U;
+    const uint32_t mn = (k + 1) / U;
+    const uint8_t* slot = ring + ((mn & 1u) * U + jn) * kWBlockBytes + lane * 16;
+    if constexpr (jn == 0) split_barrier();
+    uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
+    read_w_group<0>(slot, Wn);
+    __builtin_amdgcn_sched_barrier(0);
+    RoundsW<0, 20>::run(v, Wc);
+    __builtin_amdgcn_sched_barrier(0);
+    read_w_group<1>(slot, Wn);
+    __builtin_amdgcn_sched_barrier(0);
+    RoundsW<20, 40>::run(v, Wc);
+    __builtin_amdgcn_sched_barrier(0);
+    read_w_group<2>(slot, Wn);
+    __builtin_amdgcn_sched_barrier(0);
+    RoundsW<40, 60>::run(v, Wc);
+    __builtin_amdgcn_sched_barrier(0);
+    read_w_group<3>(slot, Wn);
+    __builtin_amdgcn_sched_barrier(0);
+    RoundsW<60, 80>::run(v, Wc);
+    const bool live = k < T;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) h[i] = live ? h[i] + v[i] : h[i];
+}
+
+// 2U blocks (two units) per consumer iteration, unrolled, so Wa/Wb keep
+// their parity and every barrier position is a compile-time constant.
+template <int U, int J>
+struct ConsumeUnits {
+    __device__ __forceinline__ static void run(uint32_t k0, uint32_t T, uint32_t (&h)[5],
+                                               uint32_t (&Wa)[80], uint32_t (&Wb)[80],
+                                               const uint8_t* ring, int lane) {
+        if constexpr (J < 2 * U) {
+            consume_block<U, J>(k0 + J, T, h, Wa, Wb, ring, lane);
+            ConsumeUnits<U, J + 1>::run(k0, T, h, Wb, Wa, ring, lane);
+        }
+    }
+};
+
+template <int U>
 __global__ __launch_bounds__(128) void sha1_split_kernel(BatchArgs A) {
-    __shared__ __attribute__((aligned(16))) uint8_t lds[kSplitRaw * kStageBytes + 2 * kWSlotBytes];
-    uint8_t* ring = lds;
-    uint8_t* wring = lds + kSplitRaw * kStageBytes;
+    __shared__ __attribute__((aligned(16))) uint8_t ring[2 * U * kWBlockBytes];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    const WaveChunks c = wave_setup(A, blockIdx.x, lane);
-    const uint32_t T = c.valid ? total_blocks(c.en.len) : 0u;
+    const uint32_t e = blockIdx.x * 64u + (uint32_t)lane;
+    const bool valid = e < A.n;
+    Entry en = fetch_entry(A, valid ? e : blockIdx.x * 64u);
+    if (!valid) en.len = 0;
+    const uint32_t T = valid ? total_blocks(en.len) : 0u;
     const uint32_t Tmax = __builtin_amdgcn_readfirstlane(wave_max(T));
-    const uint32_t S = c.bulk;
+    // Both waves run whole units (2U blocks per consumer iteration); blocks
+    // past a lane's T are computed on stale data and never committed.
+    const uint32_t units = (Tmax + 2 * U - 1) / (2 * U) * 2;
 
     if (wave == 1) {
         // ----------------------------- producer -------------------------
-        RawRing rr;
-        if (S > 0) {
-            rr.setup(c.en.p, lane);
-#pragma unroll
-            for (int s = 0; s < kSplitRaw - 1; ++s)
-                if ((uint32_t)s < S) rr.issue(lds_addr(ring), s, s);
+        // Bulk: stages (2 full blocks) that every lane has, when every lane's
+        // chunk is 16-byte aligned (branch-free loads hipcc can count);
+        // registers hold the current stage and the next one in flight.
+        const bool a16 = (reinterpret_cast<uintptr_t>(en.p) & 15u) == 0;
+        const uint32_t S = wave_all(!valid || a16)
+                               ? __builtin_amdgcn_readfirstlane(
+                                     wave_min(valid ? (en.len >> 7) : 0xffffffffu))
+                               : 0u;
+        Stage A0, A1;
+        if (S > 0) load_stage(en.p, A0);
+        if (S > 1) load_stage(en.p + 128, A1);
+        uint32_t s = 0;
+        for (; s + 1 < S; s += 2) {
+            produce_stage<U>(en, s, S, A0, ring, lane);
+            produce_stage<U>(en, s + 1, S, A1, ring, lane);
         }
-        const uint32_t nfull = c.en.len >> 6, rem = c.en.len & 63u;
-        const uint64_t bits = (uint64_t)c.en.len * 8ull;
-        int buf = 0;
-        for (uint32_t k = 0; k < Tmax; ++k) {
+        if (s < S) produce_stage<U>(en, s, S, A0, ring, lane);
+        for (uint32_t k = 2 * S; k < units * U; ++k) {
             uint32_t w[16];
-            if (k < 2u * S) {
-                const uint32_t s = k >> 1;
-                const int half = (int)(k & 1u);
-                if (half == 0) {
-                    const uint32_t pre = s + kSplitRaw - 1;
-                    if (pre < S) {
-                        int pbuf = buf + kSplitRaw - 1;
-                        if (pbuf >= kSplitRaw) pbuf -= kSplitRaw;
-                        rr.issue(lds_addr(ring), pbuf, pre);
-                    }
-                    const uint32_t left = S - 1 - s;
-                    wait_stages(left < (uint32_t)(kSplitRaw - 1) ? (int)left : kSplitRaw - 1);
-                }
-                rr.read(ring, buf, half, lane, w);
-#pragma unroll
-                for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
-                if (half == 1 && ++buf == kSplitRaw) buf = 0;
-            } else if (k < nfull) {
-                load_block_full(c.en.p + 64ull * k, w);
-#pragma unroll
-                for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
-            } else if (k == nfull) {
-                if (rem) {
-                    load_block_partial(c.en.p + 64ull * k, rem, w);
-                } else {
-#pragma unroll
-                    for (int j = 0; j < 16; ++j) w[j] = 0u;
-                }
-#pragma unroll
-                for (int j = 0; j < 16; ++j) w[j] = pad_word(bswap(w[j]), j, (int)rem);
-                if (rem < 56u) {
-                    w[14] = (uint32_t)(bits >> 32);
-                    w[15] = (uint32_t)bits;
-                }
-            } else {
-#pragma unroll
-                for (int j = 0; j < 14; ++j) w[j] = 0u;
-                w[14] = (uint32_t)(bits >> 32);
-                w[15] = (uint32_t)bits;
-            }
-            SchedWrite<0>::run(w, wring + (k & 1u) * kWSlotBytes, lane);
-            split_barrier();
+            if (k < T) tail_block_words(en, k, w);
+            produce_block<U>(k, w, ring, lane);
         }
+        split_barrier();  // matches the consumer's last (unused) read
     } else {
         // ----------------------------- consumer -------------------------
         uint32_t h[5];
         init_state(h);
-        for (uint32_t k = 0; k < Tmax; ++k) {
-            split_barrier();
-            const uint8_t* slot = wring + (k & 1u) * kWSlotBytes + lane * 16;
-            uint32_t W[80];
-#pragma unroll
-            for (int q = 0; q < 20; ++q) {
-                const uint4 x = *reinterpret_cast<const uint4*>(slot + q * 1024);
-                W[4 * q + 0] = x.x;
-                W[4 * q + 1] = x.y;
-                W[4 * q + 2] = x.z;
-                W[4 * q + 3] = x.w;
-            }
-            uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
-            RoundsW<0>::run(v, W);
-            const bool live = k < T;
-#pragma unroll
-            for (int i = 0; i < 5; ++i) h[i] = live ? h[i] + v[i] : h[i];
+        uint32_t Wa[80], Wb[80];
+        split_barrier();  // B_0
+        read_w_group<0>(ring + lane * 16, Wa);
+        read_w_group<1>(ring + lane * 16, Wa);
+        read_w_group<2>(ring + lane * 16, Wa);
+        read_w_group<3>(ring + lane * 16, Wa);
+        for (uint32_t k = 0; k < units * U; k += 2 * U) {
+            ConsumeUnits<U, 0>::run(k, T, h, Wa, Wb, ring, lane);
         }
-        if (c.valid) emit(A, c.en.id, h);
+        if (valid) emit(A, en.id, h);
     }
 }
 
@@ -472,10 +600,15 @@ hipError_t launch_fused(const BatchArgs& A, hipStream_t st) {
     return hipGetLastError();
 }
 
-hipError_t launch_split(const BatchArgs& A, hipStream_t st) {
+hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     if (A.n == 0) return hipSuccess;
     const uint32_t groups = (A.n + 63u) / 64u;
-    hipLaunchKernelGGL(sha1_split_kernel, dim3(groups), dim3(128), 0, st, A);
+    switch (unit_blocks) {
+    case 1: hipLaunchKernelGGL(sha1_split_kernel<1>, dim3(groups), dim3(128), 0, st, A); break;
+    case 2: hipLaunchKernelGGL(sha1_split_kernel<2>, dim3(groups), dim3(128), 0, st, A); break;
+    case 3: hipLaunchKernelGGL(sha1_split_kernel<3>, dim3(groups), dim3(128), 0, st, A); break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
 

@@ -13,6 +13,7 @@
 #include <cerrno>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <numeric>
@@ -175,24 +176,35 @@ int get_device(Device** out) {
 int choose_kernel(int kernel, size_t n, int cus) {
     if (kernel != SHA1CHUNK_KERNEL_AUTO) return kernel;
     const size_t groups = (n + 63) / 64;
-    return groups <= size_t(cus) * 4 ? SHA1CHUNK_KERNEL_SPLIT : SHA1CHUNK_KERNEL_FUSED;
+    return groups <= size_t(cus) * 2 ? SHA1CHUNK_KERNEL_SPLIT : SHA1CHUNK_KERNEL_LANE;
 }
 
-hipError_t launch(int kernel, const BatchArgs& A, hipStream_t st) {
+// Split-kernel unit size: fewer barriers while one workgroup per CU leaves
+// LDS to spare; 40 KiB units once several workgroups share a CU.
+int split_unit(size_t n, int cus) {
+    if (const char* e = getenv("SHA1CHUNK_SPLIT_UNIT")) {
+        const int u = atoi(e);
+        if (u >= 1 && u <= 3) return u;
+    }
+    const size_t groups = (n + 63) / 64;
+    return groups <= size_t(cus) ? 3 : 1;
+}
+
+hipError_t launch(int kernel, const BatchArgs& A, int cus, hipStream_t st) {
     switch (kernel) {
     case SHA1CHUNK_KERNEL_LANE: return launch_lane(A, st);
     case SHA1CHUNK_KERNEL_FUSED: return launch_fused(A, st);
-    case SHA1CHUNK_KERNEL_SPLIT: return launch_split(A, st);
+    case SHA1CHUNK_KERNEL_SPLIT: return launch_split(A, split_unit(A.n, cus), st);
     default: return hipErrorInvalidValue;
     }
 }
 
-int launch_checked(int kernel, const BatchArgs& A, hipStream_t st) {
+int launch_checked(int kernel, const BatchArgs& A, hipStream_t st, int cus = 256) {
     if (kernel < SHA1CHUNK_KERNEL_LANE || kernel > SHA1CHUNK_KERNEL_SPLIT)
         return fail(SHA1CHUNK_EINVAL, "unknown kernel id %d", kernel);
     if (A.n > 0 && (reinterpret_cast<uintptr_t>(A.dig) & 3u))
         return fail(SHA1CHUNK_EALIGN, "digest buffer must be 4-byte aligned");
-    hipError_t e = launch(kernel, A, st);
+    hipError_t e = launch(kernel, A, cus, st);
     if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return SHA1CHUNK_OK;
 }
@@ -233,7 +245,7 @@ int stage_and_launch(Device& D, Slot& s, const uint8_t* base, const uint64_t* of
     A.dig = static_cast<uint8_t*>(s.ddig.p);
     // Offsets in the staged buffer are relative to its start; entries are
     // already in length order, so no order[] indirection is needed.
-    if ((rc = launch_checked(choose_kernel(SHA1CHUNK_KERNEL_AUTO, m, D.cus), A, s.stream)))
+    if ((rc = launch_checked(choose_kernel(SHA1CHUNK_KERNEL_AUTO, m, D.cus), A, s.stream, D.cus)))
         return rc;
     HIP_TRY(hipMemcpyAsync(s.hdig.p, s.ddig.p, m * 20, hipMemcpyDeviceToHost, s.stream));
     HIP_TRY(hipEventRecord(s.done, s.stream));
@@ -359,7 +371,7 @@ int sha1chunk_hash_device_async(const void* d_base, const uint64_t* d_offsets,
     A.len = d_lengths;
     A.n = static_cast<uint32_t>(n);
     A.dig = d_digests;
-    return launch_checked(choose_kernel(kernel, n, D->cus), A, static_cast<hipStream_t>(stream));
+    return launch_checked(choose_kernel(kernel, n, D->cus), A, static_cast<hipStream_t>(stream), D->cus);
 }
 
 int sha1chunk_hash_uniform_async(const void* d_base, uint32_t chunk_len, size_t n,
@@ -374,7 +386,7 @@ int sha1chunk_hash_uniform_async(const void* d_base, uint32_t chunk_len, size_t 
     A.ulen = chunk_len;
     A.n = static_cast<uint32_t>(n);
     A.dig = d_digests;
-    return launch_checked(choose_kernel(kernel, n, D->cus), A, static_cast<hipStream_t>(stream));
+    return launch_checked(choose_kernel(kernel, n, D->cus), A, static_cast<hipStream_t>(stream), D->cus);
 }
 
 int sha1chunk_compare_device_async(const uint8_t* d_digests, const uint8_t* d_expected, size_t n,
@@ -495,7 +507,7 @@ long sha1chunk_hash_stream(sha1chunk_reader_fn reader, void* reader_ctx, sha1chu
         A.len = reinterpret_cast<const uint32_t*>(d + m * 8);
         A.n = static_cast<uint32_t>(m);
         A.dig = static_cast<uint8_t*>(s.ddig.p);
-        if ((rc = launch_checked(choose_kernel(SHA1CHUNK_KERNEL_AUTO, m, D->cus), A, s.stream)))
+        if ((rc = launch_checked(choose_kernel(SHA1CHUNK_KERNEL_AUTO, m, D->cus), A, s.stream, D->cus)))
             return rc;
         HIP_TRY(hipMemcpyAsync(s.hdig.p, s.ddig.p, m * 20, hipMemcpyDeviceToHost, s.stream));
         HIP_TRY(hipEventRecord(s.done, s.stream));

@@ -211,7 +211,7 @@ def test_unaligned_device_offsets(pkg, dev, oracle, kernel):
     lens = rng.integers(0, 300000, n).astype(np.uint32)
     lens[:64] = 262144 + rng.integers(0, 200, 64)  # one wave of long chunks
     off = np.zeros(n, np.uint64)
-    off[1:] = np.cumsum(lens.astype(np.uint64) + rng.integers(0, 17, n - 1).astype(np.uint64)
+    off[1:] = np.cumsum(lens.astype(np.uint64) + rng.integers(0, 17, n).astype(np.uint64)
                         + 1)[: n - 1]
     off += 5
     host = rng.integers(0, 256, int(off[-1] + lens[-1]) + 64, dtype=np.uint8)

@@ -1,0 +1,48 @@
+#!/bin/bash
+# One GPU session on the gpurun box.  Every GPU step has its own time limit;
+# a step that crashes, aborts or times out ends the session (nothing more
+# touches the GPU); ordinary test failures (pytest rc 1) do not.
+#   usage: tools/gpu_session.sh <tag> [steps...]   steps: test sweep bench prof pmc
+set -u
+TAG=${1:-r01}
+shift || true
+STEPS=${*:-"test sweep bench prof"}
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+fatal() { [ "$1" -ge 124 ] || [ "$1" -eq 0 -a 1 -eq 0 ]; }
+
+run() {  # name limit cmd...
+    local name=$1 lim=$2
+    shift 2
+    echo "== $name ($(date +%T))"
+    timeout -k 10 "$lim" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "   rc=$rc"
+    tail -n 5 "$OUT/$name.log"
+    if [ $rc -ge 124 ] || [ $rc -eq 134 ] || [ $rc -eq 139 ]; then
+        echo "FATAL step $name rc=$rc: stopping"
+        exit $rc
+    fi
+    return 0
+}
+
+rocminfo 2>/dev/null | grep -m1 -E "gfx950" > "$OUT/arch.txt"
+nproc > "$OUT/nproc.txt"; lscpu | grep -E "Model name|^CPU\(s\)" >> "$OUT/nproc.txt"
+
+for s in $STEPS; do
+    case $s in
+    test)  run pytest_gpu 900 python -m pytest tests -q -m gpu -p no:cacheprovider --timeout 600 ;;
+    smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    sweep) run sweep 600 python tools/sweep.py --chunks 1024,4096,16384,65536,131072 --rounds 2 --out "$OUT/sweep.json" ;;
+    bench) run bench 600 python bench.py --steps 10 --warmup 2 ;;
+    prof)  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
+               python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+    pmc)   run pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
+               python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
+           run pmc2 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
+               python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    *) echo "unknown step $s" ;;
+    esac
+done
+echo "session done"

@@ -41,10 +41,15 @@ def main():
             for k in kernels:
                 dig = torch.zeros((n, 20), dtype=torch.uint8, device="cuda")
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                name = k
+                if k.startswith("split") and k[5:].isdigit():  # split<U>: force the unit size
+                    os.environ["SHA1CHUNK_SPLIT_UNIT"] = k[5:]
+                    name = "split"
                 e0.record()
-                pkg.hash_uniform_device(buf, L, n, dig, kernel=k)
+                pkg.hash_uniform_device(buf, L, n, dig, kernel=name)
                 e1.record()
                 torch.cuda.synchronize()
+                os.environ.pop("SHA1CHUNK_SPLIT_UNIT", None)
                 times[k].append(e0.elapsed_time(e1))
                 d = dig.cpu().numpy()
                 if ref is None:
