@@ -11,18 +11,21 @@
 //   sha1_lane_kernel   each lane loads its own blocks from HBM (any byte
 //                      alignment, any length); also the streaming kernel
 //                      behind SHA1Update/SHA1Final (init state + no-final).
-//   sha1_fused_kernel  one wave per 64 chunks; the wave pulls 128 contiguous
-//                      bytes of each chunk per stage with global_load_lds
-//                      (16 B/lane, 8 lanes per chunk = whole 128-B lines)
-//                      into an XOR-swizzled LDS ring, each lane reads its
-//                      own row back conflict-free; schedule + rounds in VGPRs.
+//   sha1_fused_kernel  one wave per 64 chunks, schedule + rounds in VGPRs
+//                      (~627 instructions per block), two 128-byte stages of
+//                      each chunk prefetched per lane.  The high-occupancy
+//                      kernel: >= 2 groups of 64 chunks per CU.
 //   sha1_split_kernel  workgroup = producer wave + consumer wave on the same
-//                      64 chunks.  The producer streams the blocks (same LDS
-//                      ring), byte-swaps and expands the 80-word schedule into
-//                      an LDS W-ring; the consumer runs only the 80 rounds.
-//                      This halves the serial instruction stream per chunk
-//                      when there are too few chunks to fill the SIMDs
-//                      (BASELINE config 2: 4096 chunks = 64 waves).
+//                      64 chunks.  The producer streams and byte-swaps the
+//                      blocks and expands the 80-word schedule into an LDS
+//                      ring; the consumer runs only the 80 rounds (~438
+//                      instructions per block instead of ~627), which is the
+//                      bound when there are too few chunks to fill the
+//                      SIMDs (BASELINE config 2: 4096 chunks = 64 waves).
+//
+// Measured on MI355X (tools/microbench.hip): one wave issues at
+// most one instruction per ~4.63 cycles; v_alignbit/v_add3/v_perm cost ~1.9
+// ns of SIMD time per wave-instruction vs ~1.1 ns for v_add/v_xor/v_bitop3.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -93,6 +96,7 @@ __device__ __forceinline__ void lane_loop(const Entry& en, uint32_t k0, uint32_t
 }
 
 __device__ __forceinline__ bool wave_all(bool x) { return __ballot(!x) == 0; }
+__device__ __forceinline__ bool wave_any(bool x) { return __ballot(x) != 0; }
 
 __device__ __forceinline__ void lane_blocks(const BatchArgs& A, const Entry& en, uint32_t k0,
                                             uint32_t (&h)[5]) {
@@ -106,120 +110,6 @@ __device__ __forceinline__ void lane_blocks(const BatchArgs& A, const Entry& en,
         finish_message(h, en.p + 64ull * nfull, en.len & 63u, A.prefix_bytes + en.len);
 }
 
-// ------------------------------------------------------------------------
-// LDS raw-block ring shared by the fused kernel and the split producer.
-// One stage = 2 blocks (128 B) of each of the wave's 64 chunks = 8 KiB,
-// written by 8 global_load_lds_dwordx4: instruction i covers rows 8i..8i+7,
-// lane l fetches row 8i+(l>>3), 16-B segment q = (l&7) ^ ((row>>1)&7) and
-// lands at ring + i*1024 + l*16 = row*128 + (l&7)*16.  Lane r reads its row
-// segment q at row*128 + (q ^ ((r>>1)&7))*16: every 16-lane group of a
-// ds_read_b128 then hits 16 distinct 16-B bank slots (conflict-free).
-// ------------------------------------------------------------------------
-constexpr int kStageBytes = 8192;
-
-__device__ __forceinline__ uint32_t lds_addr(const void* p) {
-    return (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) void*)p;
-}
-
-struct RawRing {
-    const uint8_t* src[8];  // per-lane source for instruction i, stage 0
-    uint32_t swz;           // this lane's read swizzle ((lane>>1)&7)
-
-    __device__ __forceinline__ void setup(const uint8_t* my_p, int lane) {
-        const uint64_t mine = reinterpret_cast<uint64_t>(my_p);
-        const uint32_t lo = static_cast<uint32_t>(mine), hi = static_cast<uint32_t>(mine >> 32);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int row = 8 * i + (lane >> 3);
-            const uint32_t rlo = __shfl(lo, row), rhi = __shfl(hi, row);
-            const uint32_t q = (uint32_t)(lane & 7) ^ (uint32_t)((row >> 1) & 7);
-            src[i] = reinterpret_cast<const uint8_t*>(((uint64_t)rhi << 32) | rlo) + 16u * q;
-        }
-        swz = (uint32_t)((lane >> 1) & 7);
-    }
-
-    // The 8 LDS-DMA loads of one stage.  Issued from inline asm so that hipcc
-    // does not see them: otherwise it drains vmcnt(0) before every ds_read of
-    // the ring and the prefetch never overlaps compute.  Completion is
-    // tracked by hand with wait_stages().  M0 (the DMA's LDS base) is set
-    // and restored inside the statement.
-    __device__ __forceinline__ void issue(uint32_t ring_lds, int buf, uint32_t stage) const {
-        const uint32_t dst = __builtin_amdgcn_readfirstlane(ring_lds + (uint32_t)buf * kStageBytes);
-        const uint64_t step = 128ull * stage;
-        const uint8_t* p0 = src[0] + step;
-        const uint8_t* p1 = src[1] + step;
-        const uint8_t* p2 = src[2] + step;
-        const uint8_t* p3 = src[3] + step;
-        const uint8_t* p4 = src[4] + step;
-        const uint8_t* p5 = src[5] + step;
-        const uint8_t* p6 = src[6] + step;
-        const uint8_t* p7 = src[7] + step;
-        uint32_t keep, m;
-        asm volatile(
-            "s_mov_b32 %0, m0\n\t"
-            "s_mov_b32 m0, %10\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %2, off\n\t"
-            "s_add_u32 %1, %10, 0x400\n\t"
-            "s_mov_b32 m0, %1\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %3, off\n\t"
-            "s_add_u32 %1, %10, 0x800\n\t"
-            "s_mov_b32 m0, %1\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %4, off\n\t"
-            "s_add_u32 %1, %10, 0xc00\n\t"
-            "s_mov_b32 m0, %1\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %5, off\n\t"
-            "s_add_u32 %1, %10, 0x1000\n\t"
-            "s_mov_b32 m0, %1\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %6, off\n\t"
-            "s_add_u32 %1, %10, 0x1400\n\t"
-            "s_mov_b32 m0, %1\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %7, off\n\t"
-            "s_add_u32 %1, %10, 0x1800\n\t"
-            "s_mov_b32 m0, %1\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %8, off\n\t"
-            "s_add_u32 %1, %10, 0x1c00\n\t"
-            "s_mov_b32 m0, %1\n\t"
-            "s_nop 0\n\t"
-            "global_load_lds_dwordx4 %9, off\n\t"
-            "s_mov_b32 m0, %0"
-            : "=&s"(keep), "=&s"(m)
-            : "v"(p0), "v"(p1), "v"(p2), "v"(p3), "v"(p4), "v"(p5), "v"(p6), "v"(p7), "s"(dst)
-            : "memory", "scc");
-    }
-
-    // Little-endian words of block `half` (0/1) of the stage in buffer buf.
-    __device__ __forceinline__ void read(const uint8_t* ring, int buf, int half, int lane,
-                                         uint32_t (&w)[16]) const {
-        const uint8_t* row = ring + buf * kStageBytes + lane * 128;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const uint32_t q = (uint32_t)(4 * half + j) ^ swz;
-            const uint4 x = *reinterpret_cast<const uint4*>(row + 16u * q);
-            w[4 * j + 0] = x.x;
-            w[4 * j + 1] = x.y;
-            w[4 * j + 2] = x.z;
-            w[4 * j + 3] = x.w;
-        }
-    }
-};
-
-// Wait until at most `ahead` stages (8 LDS-DMA each) are still in flight.
-__device__ __forceinline__ void wait_stages(int ahead) {
-    if (ahead >= 2)
-        asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    else if (ahead == 1)
-        asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    else
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 __device__ __forceinline__ uint32_t wave_min(uint32_t x) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) x = min(x, (uint32_t)__shfl_xor(x, m));
@@ -229,28 +119,6 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
 #pragma unroll
     for (int m = 32; m >= 1; m >>= 1) x = max(x, (uint32_t)__shfl_xor(x, m));
     return x;
-}
-
-// Per-wave setup common to the fused kernel and the split producer/consumer.
-struct WaveChunks {
-    Entry en;
-    bool valid;
-    uint32_t bulk;  // wave-uniform number of LDS-staged stages (2 blocks each)
-};
-
-__device__ __forceinline__ WaveChunks wave_setup(const BatchArgs& A, uint32_t group, int lane) {
-    WaveChunks c;
-    const uint32_t e = group * 64u + (uint32_t)lane;
-    c.valid = e < A.n;
-    c.en = fetch_entry(A, c.valid ? e : group * 64u);
-    if (!c.valid) c.en.len = 0;
-    const bool aligned = (reinterpret_cast<uintptr_t>(c.en.p) & 15u) == 0;
-    const uint32_t stages = c.valid ? (c.en.len >> 7) : 0xffffffffu;
-    uint32_t bulk = wave_min(stages);
-    const uint64_t misaligned = __ballot(c.valid && !aligned);
-    if (misaligned) bulk = 0;
-    c.bulk = __builtin_amdgcn_readfirstlane(bulk);
-    return c;
 }
 
 }  // namespace
@@ -264,51 +132,6 @@ __global__ __launch_bounds__(256) void sha1_lane_kernel(BatchArgs A) {
     load_init(A, en.id, h);
     lane_blocks(A, en, 0, h);
     emit(A, en.id, h);
-}
-
-// --------------------------------------------------------------- fused ----
-template <int STAGES>
-__global__ __launch_bounds__(64) void sha1_fused_kernel(BatchArgs A) {
-    __shared__ __attribute__((aligned(16))) uint8_t ring[STAGES * kStageBytes];
-    const int lane = threadIdx.x;
-    const WaveChunks c = wave_setup(A, blockIdx.x, lane);
-    uint32_t h[5];
-    init_state(h);
-
-    const uint32_t S = c.bulk;
-    if (S > 0) {
-        RawRing rr;
-        rr.setup(c.en.p, lane);
-#pragma unroll
-        for (int s = 0; s < STAGES - 1; ++s)
-            if ((uint32_t)s < S) rr.issue(lds_addr(ring), s, s);
-        int buf = 0;
-        for (uint32_t s = 0; s < S; ++s) {
-            const uint32_t pre = s + STAGES - 1;
-            if (pre < S) {
-                int pbuf = buf + STAGES - 1;
-                if (pbuf >= STAGES) pbuf -= STAGES;
-                rr.issue(lds_addr(ring), pbuf, pre);
-            }
-            const uint32_t left = S - 1 - s;
-            wait_stages(left < (uint32_t)(STAGES - 1) ? (int)left : STAGES - 1);
-#pragma unroll
-            for (int half = 0; half < 2; ++half) {
-                uint32_t w[16];
-                rr.read(ring, buf, half, lane, w);
-#pragma unroll
-                for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
-                compress(h, w);
-            }
-            // The next issue overwrites this buffer: keep its reads ahead.
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            if (++buf == STAGES) buf = 0;
-        }
-    }
-    if (c.valid) {
-        lane_blocks(A, c.en, 2u * S, h);
-        emit(A, c.en.id, h);
-    }
 }
 
 // --------------------------------------------------------------- split ----
@@ -491,28 +314,50 @@ struct ConsumeUnits {
     }
 };
 
-template <int U>
-__global__ __launch_bounds__(128) void sha1_split_kernel(BatchArgs A) {
-    __shared__ __attribute__((aligned(16))) uint8_t ring[2 * U * kWBlockBytes];
+// PAIRS consumer/producer pairs per workgroup: waves 0..PAIRS-1 consume,
+// waves PAIRS..2*PAIRS-1 produce, pair p = (wave p, wave p+PAIRS).  Waves of
+// a workgroup are dealt to the CU's SIMDs cyclically, so with PAIRS = 4 each
+// SIMD hosts exactly one consumer and its own producer (the consumer keeps
+// the SIMD's issue slots it needs; the producer fills the rest).  All waves
+// share one s_barrier sequence, so the unit count is the workgroup maximum.
+template <int U, int PAIRS>
+__global__ __launch_bounds__(128 * PAIRS) void sha1_split_kernel(BatchArgs A) {
+    static_assert(PAIRS * 2 * U * kWBlockBytes <= 160 * 1024, "LDS");
+    __shared__ __attribute__((aligned(16))) uint8_t lds[PAIRS * 2 * U * kWBlockBytes];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int pair = wave % PAIRS;
+    const bool producer = wave >= PAIRS;
     const int lane = threadIdx.x & 63;
-    const uint32_t e = blockIdx.x * 64u + (uint32_t)lane;
+    uint8_t* ring = lds + pair * (2 * U * kWBlockBytes);
+    const uint32_t group = blockIdx.x * PAIRS + (uint32_t)pair;
+    const uint32_t e = group * 64u + (uint32_t)lane;
     const bool valid = e < A.n;
-    Entry en = fetch_entry(A, valid ? e : blockIdx.x * 64u);
+    Entry en = fetch_entry(A, valid ? e : min(group * 64u, A.n - 1u));
     if (!valid) en.len = 0;
     const uint32_t T = valid ? total_blocks(en.len) : 0u;
-    const uint32_t Tmax = __builtin_amdgcn_readfirstlane(wave_max(T));
+    uint32_t Tmax = __builtin_amdgcn_readfirstlane(wave_max(T));
+    if constexpr (PAIRS > 1) {
+        // workgroup max through the (not yet used) ring; the second barrier
+        // keeps producers from overwriting it before every wave has read it
+        uint32_t* slots = reinterpret_cast<uint32_t*>(lds);
+        if (!producer && lane == 0) slots[pair] = Tmax;
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PAIRS; ++q) Tmax = max(Tmax, slots[q]);
+        Tmax = __builtin_amdgcn_readfirstlane(Tmax);
+        __syncthreads();
+    }
     // Both waves run whole units (2U blocks per consumer iteration); blocks
     // past a lane's T are computed on stale data and never committed.
     const uint32_t units = (Tmax + 2 * U - 1) / (2 * U) * 2;
 
-    if (wave == 1) {
+    if (producer) {
         // ----------------------------- producer -------------------------
         // Bulk: stages (2 full blocks) that every lane has, when every lane's
         // chunk is 16-byte aligned (branch-free loads hipcc can count);
         // registers hold the current stage and the next one in flight.
         const bool a16 = (reinterpret_cast<uintptr_t>(en.p) & 15u) == 0;
-        const uint32_t S = wave_all(!valid || a16)
+        const uint32_t S = (wave_any(valid) && wave_all(!valid || a16))
                                ? __builtin_amdgcn_readfirstlane(
                                      wave_min(valid ? (en.len >> 7) : 0xffffffffu))
                                : 0u;
@@ -545,6 +390,53 @@ __global__ __launch_bounds__(128) void sha1_split_kernel(BatchArgs A) {
             ConsumeUnits<U, 0>::run(k, T, h, Wa, Wb, ring, lane);
         }
         if (valid) emit(A, en.id, h);
+    }
+}
+
+// --------------------------------------------------------------- fused ----
+// One wave, 64 chunks, schedule and rounds in registers (~630 VALU per
+// block).  Best once there are enough chunks for two or more waves per SIMD:
+// then the SIMD, not one wave's issue rate, is the limit and the split
+// kernel's LDS hand-off is pure overhead.  Each lane streams its own chunk
+// with 16-byte loads, two 128-byte stages (4 blocks) in flight in VGPRs so
+// HBM latency under full load stays covered.
+__device__ __forceinline__ void fused_stage(uint32_t s, uint32_t S, const Entry& en, Stage& cur,
+                                            uint32_t (&h)[5]) {
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        uint32_t w[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = bswap(cur.w[16 * half + j]);
+        if (half == 1 && s + 2 < S) load_stage(en.p + 128ull * (s + 2), cur);
+        compress(h, w);
+    }
+}
+
+__global__ __launch_bounds__(256) void sha1_fused_kernel(BatchArgs A) {
+    const uint32_t e = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t group = e / 64u;
+    const bool valid = e < A.n;
+    Entry en = fetch_entry(A, valid ? e : min(group * 64u, A.n - 1u));
+    if (!valid) en.len = 0;
+    uint32_t h[5];
+    init_state(h);
+    const bool a16 = (reinterpret_cast<uintptr_t>(en.p) & 15u) == 0;
+    const uint32_t S = (wave_any(valid) && wave_all(!valid || a16))
+                           ? __builtin_amdgcn_readfirstlane(
+                                 wave_min(valid ? (en.len >> 7) : 0xffffffffu))
+                           : 0u;
+    Stage A0, A1;
+    if (S > 0) load_stage(en.p, A0);
+    if (S > 1) load_stage(en.p + 128, A1);
+    uint32_t s = 0;
+    for (; s + 1 < S; s += 2) {
+        fused_stage(s, S, en, A0, h);
+        fused_stage(s + 1, S, en, A1, h);
+    }
+    if (s < S) fused_stage(s, S, en, A0, h);
+    if (valid) {
+        lane_blocks(A, en, 2u * S, h);
+        emit(A, en.id, h);
     }
 }
 
@@ -595,8 +487,7 @@ hipError_t launch_lane(const BatchArgs& A, hipStream_t st) {
 
 hipError_t launch_fused(const BatchArgs& A, hipStream_t st) {
     if (A.n == 0) return hipSuccess;
-    const uint32_t groups = (A.n + 63u) / 64u;
-    hipLaunchKernelGGL(sha1_fused_kernel<2>, dim3(groups), dim3(64), 0, st, A);
+    hipLaunchKernelGGL(sha1_fused_kernel, dim3((A.n + 255u) / 256u), dim3(256), 0, st, A);
     return hipGetLastError();
 }
 
@@ -604,9 +495,15 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     if (A.n == 0) return hipSuccess;
     const uint32_t groups = (A.n + 63u) / 64u;
     switch (unit_blocks) {
-    case 1: hipLaunchKernelGGL(sha1_split_kernel<1>, dim3(groups), dim3(128), 0, st, A); break;
-    case 2: hipLaunchKernelGGL(sha1_split_kernel<2>, dim3(groups), dim3(128), 0, st, A); break;
-    case 3: hipLaunchKernelGGL(sha1_split_kernel<3>, dim3(groups), dim3(128), 0, st, A); break;
+    case 1: hipLaunchKernelGGL((sha1_split_kernel<1, 1>), dim3(groups), dim3(128), 0, st, A); break;
+    case 2: hipLaunchKernelGGL((sha1_split_kernel<2, 1>), dim3(groups), dim3(128), 0, st, A); break;
+    case 3: hipLaunchKernelGGL((sha1_split_kernel<3, 1>), dim3(groups), dim3(128), 0, st, A); break;
+    case 4:  // 4 pairs per workgroup (512 threads), one consumer + producer per SIMD
+        hipLaunchKernelGGL((sha1_split_kernel<1, 4>), dim3((groups + 3) / 4), dim3(512), 0, st, A);
+        break;
+    case 5:  // 2 pairs per workgroup, 2-block units
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2>), dim3((groups + 1) / 2), dim3(256), 0, st, A);
+        break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

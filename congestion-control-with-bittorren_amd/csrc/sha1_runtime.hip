@@ -169,25 +169,32 @@ int get_device(Device** out) {
     return SHA1CHUNK_OK;
 }
 
-// Pick the kernel for a batch of n chunks on a device with `cus` CUs.  The
-// split kernel halves each chunk's serial instruction stream but needs two
-// waves per 64 chunks; once there are enough chunks to give every SIMD two
-// waves of its own, the fused kernel does the same work with less LDS traffic.
+// Pick the kernel for a batch of n chunks on a device with `cus` CUs
+// (crossovers measured on MI355X, DESIGN.md "Kernel selection"):
+//  - up to 2 groups of 64 chunks per CU, each chunk's serial instruction
+//    stream is the bound: the split kernel (rounds-only consumer wave, its
+//    producer on another SIMD) is ~1.4x the fused kernel per chunk;
+//  - beyond that the SIMDs are busy and the split kernel's LDS hand-off and
+//    barriers cost more than they save: the fused kernel (schedule + rounds
+//    in one wave, 4 blocks of register prefetch) wins.
 int choose_kernel(int kernel, size_t n, int cus) {
     if (kernel != SHA1CHUNK_KERNEL_AUTO) return kernel;
     const size_t groups = (n + 63) / 64;
-    return groups <= size_t(cus) * 2 ? SHA1CHUNK_KERNEL_SPLIT : SHA1CHUNK_KERNEL_LANE;
+    return groups <= size_t(cus) * 2 ? SHA1CHUNK_KERNEL_SPLIT : SHA1CHUNK_KERNEL_FUSED;
 }
 
-// Split-kernel unit size: fewer barriers while one workgroup per CU leaves
-// LDS to spare; 40 KiB units once several workgroups share a CU.
+// Split-kernel shape: 3-block units (1 barrier per 3 blocks, 120 KiB LDS) at
+// one workgroup per CU, 2-block units (80 KiB) at two per CU, else 1-block
+// units (40 KiB).  SHA1CHUNK_SPLIT_UNIT overrides (1..5, see launch_split).
 int split_unit(size_t n, int cus) {
     if (const char* e = getenv("SHA1CHUNK_SPLIT_UNIT")) {
         const int u = atoi(e);
-        if (u >= 1 && u <= 3) return u;
+        if (u >= 1 && u <= 5) return u;
     }
     const size_t groups = (n + 63) / 64;
-    return groups <= size_t(cus) ? 3 : 1;
+    if (groups <= size_t(cus)) return 3;
+    if (groups <= size_t(cus) * 2) return 2;
+    return 1;
 }
 
 hipError_t launch(int kernel, const BatchArgs& A, int cus, hipStream_t st) {

@@ -7,6 +7,8 @@
 #include <stdio.h>
 #include <stdlib.h>
 
+#include "../congestion-control-with-bittorren_amd/csrc/sha1_device.hpp"
+
 #define CHECK(x)                                                                   \
     do {                                                                           \
         hipError_t e = (x);                                                        \
@@ -100,8 +102,9 @@ __global__ void issue_kernel(uint32_t* out, uint64_t* stamps, int iters) {
         }                                                                                \
         __builtin_amdgcn_sched_barrier(0);                                               \
         const uint64_t t1 = memtime();                                                   \
-        out[threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7;                        \
-        if (threadIdx.x == 0) stamps[0] = t1 - t0;                                       \
+        out[blockIdx.x * blockDim.x + threadIdx.x] = r0 ^ r1 ^ r2 ^ r3 ^ r4 ^ r5 ^ r6 ^ r7; \
+        if ((threadIdx.x & 63) == 0)                                                     \
+            stamps[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = t1 - t0;              \
     }
 #define A_ADD(i) "v_add_u32 %" #i ", %" #i ", %8\n\t"
 #define A_ADD3(i) "v_add3_u32 %" #i ", %" #i ", %8, %9\n\t"
@@ -157,6 +160,166 @@ static void run_op(const char* name, void (*k)(uint32_t*, uint64_t*, int)) {
     CHECK(hipFree(st));
 }
 
+
+// Round mix with explicit registers: BANKS=0 -> every 3-source op reads three
+// different banks (v40..v47 chosen by bank); BANKS=1 -> all sources in one
+// bank (v40, v44, v48, v52 ...).
+template <int BANKS>
+__global__ void bank_kernel(uint32_t* out, uint64_t* stamps, int iters) {
+    const uint64_t t0 = memtime();
+    for (int i = 0; i < iters; ++i) {
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            if constexpr (BANKS == 0) {
+                asm volatile(
+                    "v_alignbit_b32 v45, v40, v40, 27\n\t"
+                    "v_bitop3_b32 v46, v41, v42, v43 bitop3:0x96\n\t"
+                    "v_add3_u32 v47, v44, v49, v50\n\t"
+                    "v_add3_u32 v44, v45, v46, v47\n\t"
+                    "v_alignbit_b32 v41, v41, v41, 2\n\t"
+                    "v_alignbit_b32 v45, v44, v44, 27\n\t"
+                    "v_bitop3_b32 v46, v40, v41, v42 bitop3:0x96\n\t"
+                    "v_add3_u32 v47, v43, v49, v50\n\t"
+                    "v_add3_u32 v43, v45, v46, v47\n\t"
+                    "v_alignbit_b32 v40, v40, v40, 2" ::: "v40", "v41", "v42", "v43", "v44",
+                    "v45", "v46", "v47", "v49", "v50");
+            } else {
+                asm volatile(
+                    "v_alignbit_b32 v60, v40, v40, 27\n\t"
+                    "v_bitop3_b32 v64, v44, v48, v52 bitop3:0x96\n\t"
+                    "v_add3_u32 v68, v56, v72, v76\n\t"
+                    "v_add3_u32 v56, v60, v64, v68\n\t"
+                    "v_alignbit_b32 v44, v44, v44, 2\n\t"
+                    "v_alignbit_b32 v60, v56, v56, 27\n\t"
+                    "v_bitop3_b32 v64, v40, v44, v48 bitop3:0x96\n\t"
+                    "v_add3_u32 v68, v52, v72, v76\n\t"
+                    "v_add3_u32 v52, v60, v64, v68\n\t"
+                    "v_alignbit_b32 v40, v40, v40, 2" ::: "v40", "v44", "v48", "v52", "v56",
+                    "v60", "v64", "v68", "v72", "v76");
+            }
+        }
+    }
+    const uint64_t t1 = memtime();
+    out[blockIdx.x * blockDim.x + threadIdx.x] = 0;
+    if ((threadIdx.x & 63) == 0) stamps[(blockIdx.x * blockDim.x + threadIdx.x) >> 6] = t1 - t0;
+}
+
+template <int BANKS>
+static void run_bank(const char* name, int blocks, int threads) {
+    const int iters = 2000, waves = blocks * threads / 64;
+    uint32_t* out;
+    uint64_t* st;
+    CHECK(hipMalloc(&out, 4 * blocks * threads));
+    CHECK(hipMalloc(&st, 8 * waves));
+    hipLaunchKernelGGL(bank_kernel<BANKS>, dim3(blocks), dim3(threads), 0, 0, out, st, 10);
+    CHECK(hipDeviceSynchronize());
+    hipLaunchKernelGGL(bank_kernel<BANKS>, dim3(blocks), dim3(threads), 0, 0, out, st, iters);
+    CHECK(hipDeviceSynchronize());
+    uint64_t* h = (uint64_t*)malloc(8 * waves);
+    CHECK(hipMemcpy(h, st, 8 * waves, hipMemcpyDeviceToHost));
+    double c = 0;
+    for (int w = 0; w < waves; ++w) c += (double)h[w];
+    c /= waves;
+    printf("{\"bank_test\": \"%s\", \"waves_per_simd\": %d, \"cycles_per_instr_per_wave\": %.3f}\n", name,
+           threads / 256 > 0 ? threads / 256 : 1, c / (iters * 16.0 * 10));
+    free(h);
+    CHECK(hipFree(out));
+    CHECK(hipFree(st));
+}
+
+
+// The real compression (schedule + 80 rounds, ~613 VALU) on register data,
+// no memory traffic: isolates the VALU mix from the load path.
+__global__ void compress_kernel(uint32_t* out, uint64_t* stamps, int iters) {
+    uint32_t h[5];
+    s1::init_state(h);
+    uint32_t seed = threadIdx.x * 0x9e3779b9u + blockIdx.x;
+    const uint64_t t0 = memtime(), q0 = realtime();
+    for (int i = 0; i < iters; ++i) {
+        uint32_t w[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = s1::bswap(seed + j * 0x01000193u + (uint32_t)i);
+        s1::compress(h, w);
+        seed ^= h[0];
+    }
+    const uint64_t t1 = memtime(), q1 = realtime();
+    out[blockIdx.x * blockDim.x + threadIdx.x] = h[0] ^ h[1] ^ h[2] ^ h[3] ^ h[4];
+    if ((threadIdx.x & 63) == 0) {
+        const int w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+        stamps[2 * w] = t1 - t0;
+        stamps[2 * w + 1] = q1 - q0;
+    }
+}
+
+static void run_compress(int blocks, int threads) {
+    const int iters = 400, waves = blocks * threads / 64;
+    uint32_t* out;
+    uint64_t* st;
+    CHECK(hipMalloc(&out, 4 * blocks * threads));
+    CHECK(hipMalloc(&st, 16 * waves));
+    hipLaunchKernelGGL(compress_kernel, dim3(blocks), dim3(threads), 0, 0, out, st, 4);
+    CHECK(hipDeviceSynchronize());
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    CHECK(hipEventRecord(e0));
+    hipLaunchKernelGGL(compress_kernel, dim3(blocks), dim3(threads), 0, 0, out, st, iters);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipDeviceSynchronize());
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    uint64_t* h = (uint64_t*)malloc(16 * waves);
+    CHECK(hipMemcpy(h, st, 16 * waves, hipMemcpyDeviceToHost));
+    double c = 0, q = 0;
+    for (int w = 0; w < waves; ++w) {
+        c += (double)h[2 * w];
+        q += (double)h[2 * w + 1];
+    }
+    c /= waves;
+    q /= waves;
+    const double lanes = (double)blocks * threads;
+    printf("{\"compress_test\": \"%d x %d\", \"cycles_per_block_per_wave\": %.1f, "
+           "\"clock_ghz\": %.3f, \"wave_ms\": %.3f, \"kernel_ms\": %.3f, \"GBps_equiv\": %.1f}\n",
+           blocks, threads, c / iters, c / q * 0.1, q * 1e-5, ms,
+           lanes * 64.0 * iters / (ms * 1e-3) / 1e9);
+    free(h);
+    CHECK(hipFree(out));
+    CHECK(hipFree(st));
+}
+
+
+static void run_op_full(const char* name, void (*k)(uint32_t*, uint64_t*, int), int blocks, int threads) {
+    const int iters = 1000, waves = blocks * threads / 64;
+    uint32_t* out;
+    uint64_t* st;
+    CHECK(hipMalloc(&out, 4 * blocks * threads));
+    CHECK(hipMalloc(&st, 8 * waves));
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(threads), 0, 0, out, st, 10);
+    CHECK(hipDeviceSynchronize());
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    CHECK(hipEventRecord(e0));
+    hipLaunchKernelGGL(k, dim3(blocks), dim3(threads), 0, 0, out, st, iters);
+    CHECK(hipEventRecord(e1));
+    CHECK(hipDeviceSynchronize());
+    float ms;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    uint64_t* h = (uint64_t*)malloc(8 * waves);
+    CHECK(hipMemcpy(h, st, 8 * waves, hipMemcpyDeviceToHost));
+    double c = 0;
+    for (int w = 0; w < waves; ++w) c += (double)h[w];
+    c /= waves;
+    const double n = iters * 16.0 * 8;
+    const double simd_instr = (double)waves / 1024.0 * n;  // wave-instructions per SIMD
+    printf("{\"op_full\": \"%s\", \"waves_per_simd\": %d, \"cyc_per_instr_per_wave\": %.3f, "
+           "\"ns_per_simd_instr\": %.4f, \"clock_ghz\": %.3f}\n",
+           name, waves / 1024, c / n, ms * 1e6 / simd_instr, c / (ms * 1e-3) / 1e9);
+    free(h);
+    CHECK(hipFree(out));
+    CHECK(hipFree(st));
+}
+
 template <int MODE>
 static void run(const char* name, int blocks, int threads, int instr_per_iter) {
     const int iters = 2000;
@@ -188,6 +351,33 @@ static void run(const char* name, int blocks, int threads, int instr_per_iter) {
 }
 
 int main() {
+    run_op_full("v_add_u32", op_add, 256, 1024);
+    run_op_full("v_xor_b32", op_xor, 256, 1024);
+    run_op_full("v_add3_u32", op_add3, 256, 1024);
+    run_op_full("v_bitop3_b32", op_bitop3, 256, 1024);
+    run_op_full("v_alignbit_b32", op_alignbit, 256, 1024);
+    run_op_full("v_alignbit s,s", op_align_ss, 256, 1024);
+    run_op_full("v_perm_b32", op_perm, 256, 1024);
+    run_op_full("v_bfi_b32", op_bfi, 256, 1024);
+    run_op_full("v_lshl_add_u32", op_lshl_add, 256, 1024);
+    run_op_full("v_add_u32 2/SIMD", op_add, 256, 512);
+    run_op_full("v_add3_u32 2/SIMD", op_add3, 256, 512);
+    run_op_full("v_alignbit 2/SIMD", op_alignbit, 256, 512);
+    run_op_full("v_add_u32 8/SIMD", op_add, 512, 1024);
+    run_op_full("v_add3_u32 8/SIMD", op_add3, 512, 1024);
+    run_compress(1, 64);
+    run_compress(256, 256);
+    run_compress(256, 512);
+    run_compress(256, 1024);
+    run_compress(512, 1024);
+    run_bank<0>("distinct_banks", 1, 64);
+    run_bank<1>("same_bank", 1, 64);
+    run_bank<0>("distinct_banks", 256, 256);
+    run_bank<1>("same_bank", 256, 256);
+    run_bank<0>("distinct_banks", 256, 512);
+    run_bank<1>("same_bank", 256, 512);
+    run_bank<0>("distinct_banks", 256, 1024);
+    run_bank<1>("same_bank", 256, 1024);
     run_op("v_add_u32", op_add);
     run_op("v_add3_u32", op_add3);
     run_op("v_alignbit_b32", op_alignbit);
