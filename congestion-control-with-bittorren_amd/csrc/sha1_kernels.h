@@ -29,3 +29,9 @@ hipError_t launch_synth(uint8_t* dst, const uint64_t* off, const uint32_t* lens,
                         uint64_t first, uint64_t count, uint64_t seed, hipStream_t st);
 hipError_t launch_compare(const uint8_t* dig, const uint8_t* exp, uint32_t n, uint8_t* mismatch,
                           hipStream_t st);
+
+// Longest-first order of a ragged batch (sha1_sort.hip): *d_order receives n
+// indices sorted by d_len descending; release *scratch with hipFreeAsync on
+// the same stream after the consuming kernel has been enqueued.
+hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t** d_order,
+                               void** scratch, hipStream_t st);

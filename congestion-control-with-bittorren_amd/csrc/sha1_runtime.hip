@@ -217,41 +217,79 @@ int launch_checked(int kernel, const BatchArgs& A, hipStream_t st, int cus = 256
 }
 
 // ------------------------------------------------------------ host batch --
-// Stage entries [lo, hi) of `order` (caller indices, sorted by length) into
-// slot s and launch.  Layout in the pinned / device buffer:
-//   [off: u64 x m][len: u32 x m] pad to 128 | chunk bytes (each 128-aligned)
+// Host batches go through two pipeline slots (own stream each), so the H2D
+// copy of slot b+1 overlaps the kernel of slot b.  A slot's bytes come
+// either straight from the caller's buffer (when it is pinned and the slot's
+// chunks are back to back in it: one hipMemcpyAsync, no host copy) or are
+// packed into the slot's pinned staging first.  Device layout of a slot:
+//   [off: u64 x m][len: u32 x m] pad to 128 | chunk bytes
+// Slot size scales with the batch: a pass of the kernel takes ~7 ms however
+// few chunks it has (serial per chunk), so a slot must carry enough bytes
+// that its PCIe copy, not the kernel, is the longer stage.
+size_t slot_bytes_for(uint64_t total) {
+    const size_t lo = size_t(256) << 20, hi = size_t(1) << 30;
+    return std::min(hi, std::max(lo, static_cast<size_t>(total / 4)));
+}
+
+bool host_pinned(const void* p) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return at.type == hipMemoryTypeHost;
+}
+
 int stage_and_launch(Device& D, Slot& s, const uint8_t* base, const uint64_t* offsets,
                      const uint32_t* lengths, const std::vector<uint32_t>& order, size_t lo,
-                     size_t hi, size_t data_bytes) {
+                     size_t hi, size_t data_bytes, bool src_pinned) {
     const size_t m = hi - lo;
     const size_t meta = round_up(m * (sizeof(uint64_t) + sizeof(uint32_t)), kAlign);
     int rc;
-    if ((rc = s.hpin.ensure(meta + data_bytes)) || (rc = s.dmem.ensure(meta + data_bytes)) ||
+    s.ids.assign(order.begin() + lo, order.begin() + hi);
+    // Direct mode: chunks contiguous and ascending in the pinned source, each
+    // length a multiple of 16 (keeps every device chunk 16-byte aligned).
+    bool direct = src_pinned;
+    uint64_t span0 = offsets[s.ids[0]], span = 0;
+    for (size_t j = 0; direct && j < m; ++j) {
+        const uint32_t id = s.ids[j];
+        direct = offsets[id] == span0 + span && (j + 1 == m || (lengths[id] & 15u) == 0);
+        span += lengths[id];
+    }
+    const size_t dbytes = direct ? round_up(span, kAlign) : data_bytes;
+    if ((rc = s.hpin.ensure(meta + (direct ? 0 : data_bytes))) || (rc = s.dmem.ensure(meta + dbytes)) ||
         (rc = s.hdig.ensure(m * 20)) || (rc = s.ddig.ensure(m * 20)))
         return rc;
     uint8_t* h = static_cast<uint8_t*>(s.hpin.p);
     uint64_t* hoff = reinterpret_cast<uint64_t*>(h);
     uint32_t* hlen = reinterpret_cast<uint32_t*>(h + m * sizeof(uint64_t));
-    s.ids.assign(order.begin() + lo, order.begin() + hi);
     size_t cur = meta;
     for (size_t j = 0; j < m; ++j) {
         const uint32_t id = s.ids[j];
         const uint32_t L = lengths[id];
-        hoff[j] = cur;
         hlen[j] = L;
-        if (L) memcpy(h + cur, base + offsets[id], L);
-        cur += round_up(L, kAlign);
+        if (direct) {
+            hoff[j] = meta + (offsets[id] - span0);
+        } else {
+            hoff[j] = cur;
+            if (L) memcpy(h + cur, base + offsets[id], L);
+            cur += round_up(L, kAlign);
+        }
     }
-    HIP_TRY(hipMemcpyAsync(s.dmem.p, h, cur, hipMemcpyHostToDevice, s.stream));
     uint8_t* d = static_cast<uint8_t*>(s.dmem.p);
+    if (direct) {
+        HIP_TRY(hipMemcpyAsync(d, h, meta, hipMemcpyHostToDevice, s.stream));
+        if (span) HIP_TRY(hipMemcpyAsync(d + meta, base + span0, span, hipMemcpyHostToDevice, s.stream));
+    } else {
+        HIP_TRY(hipMemcpyAsync(d, h, cur, hipMemcpyHostToDevice, s.stream));
+    }
     BatchArgs A{};
     A.base = d;
     A.off = reinterpret_cast<const uint64_t*>(d);
     A.len = reinterpret_cast<const uint32_t*>(d + m * sizeof(uint64_t));
     A.n = static_cast<uint32_t>(m);
     A.dig = static_cast<uint8_t*>(s.ddig.p);
-    // Offsets in the staged buffer are relative to its start; entries are
-    // already in length order, so no order[] indirection is needed.
+    // Entries are already in length order: no order[] indirection needed.
     if ((rc = launch_checked(choose_kernel(SHA1CHUNK_KERNEL_AUTO, m, D.cus), A, s.stream, D.cus)))
         return rc;
     HIP_TRY(hipMemcpyAsync(s.hdig.p, s.ddig.p, m * 20, hipMemcpyDeviceToHost, s.stream));
@@ -276,24 +314,29 @@ int hash_host(const uint8_t* base, const uint64_t* offsets, const uint32_t* leng
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(D->mu);
     // Longest first, so every wave of 64 gets near-equal lengths (a wave
-    // runs as long as its longest lane).
+    // runs as long as its longest lane); equal lengths keep caller order.
     std::vector<uint32_t> order(n);
     std::iota(order.begin(), order.end(), 0u);
     std::stable_sort(order.begin(), order.end(),
                      [&](uint32_t a, uint32_t b) { return lengths[a] > lengths[b]; });
+    uint64_t total = 0;
+    for (size_t i = 0; i < n; ++i) total += lengths[i];
+    const size_t slot_cap = slot_bytes_for(total);
+    const bool pinned = host_pinned(base);
     size_t lo = 0;
     int which = 0;
     while (lo < n) {
         size_t hi = lo, bytes = 0;
         while (hi < n) {
             const size_t b = round_up(lengths[order[hi]], kAlign);
-            if (hi > lo && bytes + b > kSlotBytes) break;
+            if (hi > lo && bytes + b > slot_cap) break;
             bytes += b;
             ++hi;
         }
         Slot& s = D->slot[which];
         if ((rc = drain(s, digests))) return rc;
-        if ((rc = stage_and_launch(*D, s, base, offsets, lengths, order, lo, hi, bytes))) return rc;
+        if ((rc = stage_and_launch(*D, s, base, offsets, lengths, order, lo, hi, bytes, pinned)))
+            return rc;
         lo = hi;
         which ^= 1;
     }
@@ -378,7 +421,16 @@ int sha1chunk_hash_device_async(const void* d_base, const uint64_t* d_offsets,
     A.len = d_lengths;
     A.n = static_cast<uint32_t>(n);
     A.dig = d_digests;
-    return launch_checked(choose_kernel(kernel, n, D->cus), A, static_cast<hipStream_t>(stream), D->cus);
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    // AUTO on a ragged batch: hash longest-first (sha1_sort.hip).
+    void* scratch = nullptr;
+    if (kernel == SHA1CHUNK_KERNEL_AUTO && n > 64) {
+        hipError_t e = sort_by_length_desc(d_lengths, A.n, &A.order, &scratch, st);
+        if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "length sort: %s", hipGetErrorString(e));
+    }
+    rc = launch_checked(choose_kernel(kernel, n, D->cus), A, st, D->cus);
+    if (scratch) (void)hipFreeAsync(scratch, st);
+    return rc;
 }
 
 int sha1chunk_hash_uniform_async(const void* d_base, uint32_t chunk_len, size_t n,

@@ -1,0 +1,156 @@
+#!/usr/bin/env python3
+"""Every BASELINE.json config on one MI355X, each checked against the
+reference's golden digests (tests/golden/golden.json), as one JSON document:
+
+  config2   4096 x 512 KiB device-resident                  (bench.py's workload)
+  config3   65536 x 512 KiB from PINNED host memory: H2D || hash || D2H
+            through sha1chunk_hash_batch's two-slot pipeline (end-to-end)
+  config4   one GPU's shard of 262144 x 512 KiB over 8 GPUs (32768 chunks),
+            device-resident; plus the whole 262144 on one GPU
+  config5   16384 mixed-length chunks (4 KiB .. 1 MiB), device-resident,
+            longest-first (AUTO) and unsorted
+  occupancy 65536 / 131072 device-resident (fused kernel regime)
+
+Usage: python tools/bench_configs.py [--out FILE] [--skip config3,...]
+"""
+from __future__ import annotations
+
+import argparse
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+L512 = 524288
+
+
+def timed(fn, reps=3):
+    import torch
+    ts = []
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts)), ts
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=None)
+    ap.add_argument("--skip", default="")
+    a = ap.parse_args()
+    skip = set(a.skip.split(",")) if a.skip else set()
+    import torch
+    pkg = importlib.import_module("congestion-control-with-bittorren_amd")
+    from oracle import oracle as O
+    torch.cuda.set_device(0)
+    pkg.set_device(0)
+    golden = json.load(open(os.path.join(ROOT, "tests/golden/golden.json")))
+    res = {"device": torch.cuda.get_device_name(0)}
+
+    def uniform(n, first=0, kernel="auto", reps=3):
+        buf = torch.empty(n * L512, dtype=torch.uint8, device="cuda")
+        pkg.synth_fill_device(buf, first, n, L512)
+        dig = torch.zeros((n, 20), dtype=torch.uint8, device="cuda")
+        sec, ts = timed(lambda: pkg.hash_uniform_device(buf, L512, n, dig, kernel=kernel), reps)
+        out = dig.cpu().numpy()
+        del buf
+        torch.cuda.empty_cache()
+        return sec, ts, out
+
+    def row(n, sec, ts, ok, **kw):
+        r = {"chunks": n, "bytes": n * L512, "seconds": round(sec, 6),
+             "GiBps": round(n * L512 / sec / 2**30, 2),
+             "hbm_frac": round(n * (L512 + 20) / sec / 8e12, 5),
+             "runs_s": [round(t, 6) for t in ts], "parity": ok}
+        r.update(kw)
+        print(json.dumps(r), flush=True)
+        return r
+
+    if "config2" not in skip:
+        sec, ts, d = uniform(4096)
+        res["config2"] = row(4096, sec, ts, O.digest_of_digests(d).hex() == golden["config2"]["agg"])
+
+    if "config4" not in skip:
+        per = 262144 // 8
+        sec, ts, d = uniform(per, first=per)
+        res["config4_shard"] = row(per, sec, ts,
+                                   O.digest_of_digests(d).hex() == golden["config4"]["shard_aggs"]["8"][1],
+                                   note="rank 1 of 8")
+        sec, ts, d = uniform(262144, reps=2)
+        res["config4_one_gpu"] = row(262144, sec, ts,
+                                     O.digest_of_digests(d).hex() == golden["config4"]["agg"])
+
+    if "occupancy" not in skip:
+        for n in (65536, 131072):
+            sec, ts, d = uniform(n)
+            ok = O.digest_of_digests(d).hex() == golden["config3"]["agg"] if n == 65536 else \
+                all(d[int(i)].tobytes().hex() == h for i, h in golden["config3"]["sample"].items())
+            res[f"device_{n}"] = row(n, sec, ts, ok)
+
+    if "config5" not in skip:
+        n = golden["config5"]["chunks"]
+        lens = O.mixed_lengths(n)
+        off, total = pkg.sha1chunk.ragged_layout(lens)
+        d_base = torch.zeros(total + 128, dtype=torch.uint8, device="cuda")
+        d_off = torch.from_numpy(off.astype(np.int64)).cuda()
+        d_len = torch.from_numpy(lens.astype(np.int32)).cuda()
+        pkg.synth_fill_ragged_device(d_base, d_off, d_len, 0)
+        want = np.fromfile(os.path.join(ROOT, "tests/golden/mixed_16384.bin"), np.uint8).reshape(-1, 20)
+        nbytes = int(lens.astype(np.uint64).sum())
+        longest_blocks = int(lens.max()) // 64 + 2
+        for k in ("auto", "split", "fused"):
+            dig = torch.zeros((n, 20), dtype=torch.uint8, device="cuda")
+            sec, ts = timed(lambda: pkg.hash_device(d_base, d_off, d_len, dig, kernel=k))
+            ok = bool(np.array_equal(dig.cpu().numpy(), want))
+            r = row(n, sec, ts, ok, kernel=k, payload_bytes=nbytes,
+                    payload_GiBps=round(nbytes / sec / 2**30, 2), longest_chunk_blocks=longest_blocks,
+                    sorted=(k == "auto"))
+            r["bytes"] = nbytes
+            r["GiBps"] = r["payload_GiBps"]
+            res[f"config5_{k}"] = r
+        del d_base
+        torch.cuda.empty_cache()
+
+    if "config3" not in skip:
+        n = 65536
+        host = torch.empty(n * L512, dtype=torch.uint8, pin_memory=True)
+        piece = 2048
+        tmp = torch.empty(piece * L512, dtype=torch.uint8, device="cuda")
+        for c0 in range(0, n, piece):
+            pkg.synth_fill_device(tmp, c0, piece, L512)
+            host[c0 * L512:(c0 + piece) * L512].copy_(tmp)
+        torch.cuda.synchronize()
+        del tmp
+        torch.cuda.empty_cache()
+        hv = host.numpy()
+        off = np.arange(n, dtype=np.uint64) * L512
+        ln = np.full(n, L512, np.uint32)
+        out = {}
+
+        def run():
+            out["d"] = pkg.hash_batch(hv, off, ln)
+        sec, ts = timed(run, reps=2)
+        ok = O.digest_of_digests(out["d"]).hex() == golden["config3"]["agg"]
+        res["config3_pinned_e2e"] = row(n, sec, ts, ok, mode="pinned host -> H2D || hash || D2H")
+        # raw PCIe rate on this box for the same bytes, for context
+        dev = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
+        sec_c, _ = timed(lambda: dev.copy_(host[: 1 << 30], non_blocking=True), reps=3)
+        res["pcie_h2d_GiBps"] = round(1.0 / sec_c, 2)
+        print(json.dumps({"pcie_h2d_GiBps": res["pcie_h2d_GiBps"]}), flush=True)
+        del host, dev
+
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump(res, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
