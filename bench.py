@@ -10,9 +10,17 @@ per GPU): every rank hashes its own 4096 chunks (global chunk ids
 collectives are the timing barrier and the max-over-ranks reduction.
 
 Prints ONE JSON line on rank 0 with `roofline` (dominant kernel vs the HBM
-peak, per-launch time from HIP events on the kernel's own stream) and
+peak, per-launch time from HIP events on the kernel's own stream; `traffic`
+from the committed rocprofv3 PMC pass, profiles/traffic_*.json),
+`serial_bound` (the per-chunk limit that actually binds this workload: SHA-1
+is serial inside a chunk and one wave issues one instruction per ~4.63
+cycles, so 4096 chunks = 64 waves cannot fill 1024 SIMDs) and
 `cpu_baseline` (the reference sha.c, compiled from its sources into
 oracle/_ref, timed on this host's cores on the same chunks).
+
+--streams P (default 1) keeps P independent batches in flight on P HIP
+streams (each its own 4096 distinct chunks); the default measures one batch
+at a time.
 """
 from __future__ import annotations
 
@@ -31,8 +39,13 @@ sys.path.insert(0, ROOT)
 
 METRIC = "GiB/s device-resident SHA-1 over 512KB chunks; % of HBM-read roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
-VALU_OPS_PER_BLOCK = 613  # gfx950 ISA count per 64-B compression
-VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12  # 256 CU x 4 SIMD32 x 2.4 GHz lane-ops
+# Per-chunk serial floor: a rounds-only wave needs 5 VALU per round x 80
+# rounds per 64-B block; one wave issues one instruction per 4.63 cycles
+# (measured, tools/microbench.hip -> profiles/microbench_issue_r01.json) at
+# the 2.4 GHz the chip holds at this occupancy.
+ROUND_VALU_PER_BLOCK = 400
+ISSUE_CYCLES = 4.63
+CLOCK_HZ = 2.4e9
 
 
 def parse():
@@ -43,6 +56,7 @@ def parse():
     ap.add_argument("--chunks", type=int, default=4096, help="chunks per GPU")
     ap.add_argument("--chunk-len", type=int, default=524288)
     ap.add_argument("--kernel", default="auto", choices=["auto", "lane", "fused", "split"])
+    ap.add_argument("--streams", type=int, default=1, help="independent batches in flight")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     return ap.parse_args()
@@ -62,25 +76,29 @@ def main():
     pkg = importlib.import_module("congestion-control-with-bittorren_amd")
     pkg.set_device(local)
 
-    n, L = a.chunks, a.chunk_len
-    first = rank * n  # weak scaling: each rank its own chunk ids
-    buf = torch.empty(n * L, dtype=torch.uint8, device="cuda")
-    dig = torch.zeros((n, 20), dtype=torch.uint8, device="cuda")
-    stream = torch.cuda.Stream()
-    with torch.cuda.stream(stream):
-        pkg.synth_fill_device(buf, first, n, L, stream=stream)
-    stream.synchronize()
+    shard = importlib.import_module("congestion-control-with-bittorren_amd.shard")
+    n, L, P = a.chunks, a.chunk_len, max(1, a.streams)
+    # weak scaling: rank r owns chunk ids [n*r, n*(r+1)); with P in-flight
+    # batches each batch is its own disjoint range of ids
+    first, _ = shard.weak_shard(rank * P, n)
+    bufs = [torch.empty(n * L, dtype=torch.uint8, device="cuda") for _ in range(P)]
+    digs = [torch.zeros((n, 20), dtype=torch.uint8, device="cuda") for _ in range(P)]
+    streams = [torch.cuda.Stream() for _ in range(P)]
+    for p in range(P):
+        pkg.synth_fill_device(bufs[p], first + p * n, n, L, stream=streams[p])
+    torch.cuda.synchronize()
 
-    def step(ev0=None, ev1=None):
+    def step(i, ev0=None, ev1=None):
+        p = i % P
         if ev0 is not None:
-            ev0.record(stream)
-        pkg.hash_uniform_device(buf, L, n, dig, stream=stream, kernel=a.kernel)
+            ev0.record(streams[p])
+        pkg.hash_uniform_device(bufs[p], L, n, digs[p], stream=streams[p], kernel=a.kernel)
         if ev1 is not None:
-            ev1.record(stream)
+            ev1.record(streams[p])
 
-    for _ in range(a.warmup):
-        step()
-    stream.synchronize()
+    for i in range(a.warmup):
+        step(i)
+    torch.cuda.synchronize()
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(a.steps)]
@@ -88,44 +106,39 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for e0, e1 in evs:
-        step(e0, e1)
+    for i, (e0, e1) in enumerate(evs):
+        step(i, e0, e1)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     if world > 1:
         dist.barrier()
-    elapsed = t1 - t0
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
-    if world > 1:
-        t = torch.tensor([elapsed, kern_ms], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_ms = float(t[0]), float(t[1])
+    elapsed, kern_ms = shard.max_over_ranks([t1 - t0, kern_ms], device="cuda")
 
     # ---- parity of the timed output (every rank, against the reference) ----
-    got = dig.cpu().numpy()
     from oracle import oracle as O  # checker only
     golden = json.load(open(os.path.join(ROOT, "tests/golden/golden.json")))
-    parity = None
-    if n == 4096 and L == O.CHUNK_LEN and rank < len(golden["weak4096"]):
-        parity = O.digest_of_digests(got).hex() == golden["weak4096"][rank]
-    else:
-        idx = np.unique(np.linspace(0, n - 1, min(n, 16)).astype(np.int64))
-        host = np.concatenate([O.synth_chunks(first + int(i), 1, L) for i in idx])
-        want = O.hash_batch(host, np.arange(idx.size, dtype=np.uint64) * L,
-                            np.full(idx.size, L, np.uint32))
-        parity = bool(np.array_equal(got[idx], want))
-    if world > 1:
-        ok = torch.tensor([1.0 if parity else 0.0], device="cuda")
-        dist.all_reduce(ok, op=dist.ReduceOp.MIN)
-        parity = bool(ok.item() > 0.5)
+    parity = True
+    for p in range(P):
+        got = digs[p].cpu().numpy()
+        b = first // n + p  # index of this batch's 4096-chunk range
+        if n == 4096 and L == O.CHUNK_LEN and b < len(golden["weak4096"]):
+            parity &= O.digest_of_digests(got).hex() == golden["weak4096"][b]
+        else:
+            idx = np.unique(np.linspace(0, n - 1, min(n, 16)).astype(np.int64))
+            host = np.concatenate([O.synth_chunks(first + p * n + int(i), 1, L) for i in idx])
+            want = O.hash_batch(host, np.arange(idx.size, dtype=np.uint64) * L,
+                                np.full(idx.size, L, np.uint32))
+            parity &= bool(np.array_equal(got[idx], want))
+    parity = shard.all_ranks_ok(parity, device="cuda")
 
     ms_per_step = elapsed / a.steps * 1e3
     total_bytes = world * n * L
     value = total_bytes / (elapsed / a.steps) / 2**30
     alg_bytes = n * (L + 20)  # per launch: every chunk byte read once + its digest
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
-    blocks = n * ((L + 8) // 64 + 1)
-    valu_tops = blocks * VALU_OPS_PER_BLOCK / (kern_ms * 1e-3) / 1e12
+    blocks = (L + 8) // 64 + 1  # SHA-1 compressions per chunk (sha.c:536-543 padding)
+    floor_ms = blocks * ROUND_VALU_PER_BLOCK * ISSUE_CYCLES / CLOCK_HZ * 1e3
 
     result = {
         "metric": METRIC,
@@ -141,7 +154,7 @@ def main():
         "dtype": "u32",
         "data": "synthetic (splitmix64 corpus, SURVEY.md 8d), resident in HBM",
         "config": {"workload": f"{n} x {L} B chunks per GPU, device-resident (BASELINE config 2)",
-                   "chunks_per_gpu": n, "chunk_bytes": L, "kernel": a.kernel,
+                   "chunks_per_gpu": n, "chunk_bytes": L, "kernel": a.kernel, "streams": P,
                    "parallelism": f"chunk-sharded x{world}, no collective"},
         "parity": parity,
         "roofline": {
@@ -152,9 +165,12 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": _traffic(n, L),
             "kernel_ms": round(kern_ms, 4),
-            "valu": {"achieved_tops": round(valu_tops, 3), "peak_tops": round(VALU_PEAK_TOPS, 2),
-                     "frac": round(valu_tops / VALU_PEAK_TOPS, 5),
-                     "ops_per_block": VALU_OPS_PER_BLOCK},
+        },
+        "serial_bound": {
+            "bound": "per-chunk serial VALU issue (rounds-only wave)",
+            "floor_ms": round(floor_ms, 4), "achieved_ms": round(kern_ms, 4),
+            "frac": round(floor_ms / kern_ms, 4),
+            "model": f"{blocks} blocks x {ROUND_VALU_PER_BLOCK} VALU x {ISSUE_CYCLES} cyc / 2.4 GHz",
         },
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
