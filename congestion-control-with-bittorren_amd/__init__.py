@@ -8,10 +8,10 @@ from .sha1chunk import *  # noqa: F401,F403
 from .sha1chunk import (SHA1, SHA1Context, Sha1ChunkError, binary2hex, device_count,  # noqa: F401
                         get_chunk_hash, hash_batch, hash_device, hash_uniform_device,
                         hex2binary, lib, make_chunks, set_device, shahash,
-                        synth_fill_device, verify_batch, verify_hash)
+                        synth_fill_device, verify_batch, verify_hash, VerifyQueue)
 
 __all__ = [
     "SHA1", "SHA1Context", "Sha1ChunkError", "binary2hex", "device_count", "get_chunk_hash",
     "hash_batch", "hash_device", "hash_uniform_device", "hex2binary", "lib", "make_chunks",
-    "set_device", "shahash", "synth_fill_device", "verify_batch", "verify_hash",
+    "set_device", "shahash", "synth_fill_device", "verify_batch", "verify_hash", "VerifyQueue",
 ]

@@ -44,29 +44,35 @@ __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32
 // in place: a = v[(0-t)%5] ... e = v[(4-t)%5]; the new a lands in e's slot
 // and b is rotated in its own slot, so no register moves are emitted.
 template <int T>
+__device__ __forceinline__ constexpr uint32_t round_k() {
+    return T < 20 ? K0 : T < 40 ? K1 : T < 60 ? K2 : K3;
+}
+
+// WK = true: wt already holds W[t] + K[t] (the split producer adds it), so
+// e + W + K is a 2-operand v_add_u32 (VOP2, issues ~6% faster than VOP3).
+template <int T, bool WK = false>
 __device__ __forceinline__ void round_step(uint32_t (&v)[5], uint32_t wt) {
     constexpr int ia = (5 - (T % 5)) % 5;
     constexpr int ib = (ia + 1) % 5, ic = (ia + 2) % 5, id = (ia + 3) % 5, ie = (ia + 4) % 5;
-    uint32_t f, k;
-    if constexpr (T < 20) {
+    uint32_t f;
+    if constexpr (T < 20)
         f = chf(v[ib], v[ic], v[id]);
-        k = K0;
-    } else if constexpr (T < 40) {
+    else if constexpr (T < 40)
         f = xor3(v[ib], v[ic], v[id]);
-        k = K1;
-    } else if constexpr (T < 60) {
+    else if constexpr (T < 60)
         f = maj(v[ib], v[ic], v[id]);
-        k = K2;
-    } else {
+    else
         f = xor3(v[ib], v[ic], v[id]);
-        k = K3;
-    }
     // temp = ROTL5(a) + F + e + K + W.  e + K + W does not depend on a, so it
     // is summed first, off the chain; the chain a -> {ROTL5(a), F} -> add3
     // is then 2 dependent VALU ops per round instead of 3.  The add3 is
     // pinned in asm because LLVM otherwise re-associates the 5-term sum as
     // (e + ROTL5(a) + F) + (W + K), putting both adds on the chain.
-    const uint32_t x = v[ie] + wt + k;
+    uint32_t x;
+    if constexpr (WK)
+        x = v[ie] + wt;
+    else
+        x = v[ie] + wt + round_k<T>();
     uint32_t t;
     asm("v_add3_u32 %0, %1, %2, %3" : "=v"(t) : "v"(rotl(v[ia], 5)), "v"(f), "v"(x));
     v[ie] = t;
@@ -107,14 +113,14 @@ __device__ __forceinline__ void compress(uint32_t (&h)[5], uint32_t (&w)[16]) {
     for (int i = 0; i < 5; ++i) h[i] += v[i];
 }
 
-// Rounds only, with the 80-word schedule supplied in registers (split
-// kernel consumer: the producer wave computed it).
-template <int T, int END = 80>
+// Rounds only, with W[t] + K[t] supplied in registers (split kernel
+// consumer: the producer wave computed the schedule and added K).
+template <int T, int END = 80, bool WK = true>
 struct RoundsW {
     __device__ __forceinline__ static void run(uint32_t (&v)[5], const uint32_t (&W)[80]) {
         if constexpr (T < END) {
-            round_step<T>(v, W[T]);
-            RoundsW<T + 1, END>::run(v, W);
+            round_step<T, WK>(v, W[T]);
+            RoundsW<T + 1, END, WK>::run(v, W);
         }
     }
 };

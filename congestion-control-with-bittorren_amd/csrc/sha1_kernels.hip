@@ -167,18 +167,21 @@ __device__ __forceinline__ void split_barrier() {
     asm volatile("s_barrier" ::: "memory");
 }
 
-// Producer: the 80-word schedule of one block into its W block slot.
-template <int T>
+// Producer: the 80-word schedule of one block, plus K, into its W block slot.
+template <int T, bool WK>
 struct SchedWrite {
     __device__ __forceinline__ static void run(uint32_t (&w)[16], uint8_t* slot, int lane) {
         if constexpr (T < 80) {
             if constexpr (T >= 16) sched_step<T>(w);
             if constexpr ((T & 3) == 3) {
+                // ship W + K (K is constant over each group of 4: the round
+                // ranges 0/20/40/60 are multiples of 4)
                 constexpr int j = (T - 3) & 15;
+                constexpr uint32_t k = WK ? round_k<T>() : 0u;
                 *reinterpret_cast<uint4*>(slot + (T >> 2) * 1024 + lane * 16) =
-                    make_uint4(w[j], w[j + 1], w[j + 2], w[j + 3]);
+                    make_uint4(w[j] + k, w[j + 1] + k, w[j + 2] + k, w[j + 3] + k);
             }
-            SchedWrite<T + 1>::run(w, slot, lane);
+            SchedWrite<T + 1, WK>::run(w, slot, lane);
         }
     }
 };
@@ -218,10 +221,10 @@ __device__ __forceinline__ void tail_block_words(const Entry& en, uint32_t k, ui
     }
 }
 
-template <int U>
+template <int U, bool WK>
 __device__ __forceinline__ void produce_block(uint32_t k, uint32_t (&w)[16], uint8_t* ring, int lane) {
     const uint32_t m = k / U, j = k - m * U;
-    SchedWrite<0>::run(w, ring + ((m & 1u) * U + j) * kWBlockBytes, lane);
+    SchedWrite<0, WK>::run(w, ring + ((m & 1u) * U + j) * kWBlockBytes, lane);
     if (j == U - 1) split_barrier();
 }
 
@@ -242,7 +245,7 @@ __device__ __forceinline__ void load_stage(const uint8_t* p, Stage& st) {
 
 // Producer side of one bulk stage: blocks 2s, 2s+1 from `cur`; once the
 // second block's words are taken, `cur` is refilled with stage s+2.
-template <int U>
+template <int U, bool WK>
 __device__ __forceinline__ void produce_stage(const Entry& en, uint32_t s, uint32_t S, Stage& cur,
                                               uint8_t* ring, int lane) {
 #pragma unroll
@@ -251,7 +254,7 @@ __device__ __forceinline__ void produce_stage(const Entry& en, uint32_t s, uint3
 #pragma unroll
         for (int j = 0; j < 16; ++j) w[j] = bswap(cur.w[16 * half + j]);
         if (half == 1 && s + 2 < S) load_stage(en.p + 128ull * (s + 2), cur);
-        produce_block<U>(2 * s + half, w, ring, lane);
+        produce_block<U, WK>(2 * s + half, w, ring, lane);
     }
 }
 
@@ -270,31 +273,34 @@ __device__ __forceinline__ void read_w_group(const uint8_t* slot, uint32_t (&W)[
 // Consumer: rounds of block k from Wc while W(k+1) streams into Wn.  All of
 // it is straight-line (the barrier position is a compile-time function of
 // the unrolled block index), so hipcc inserts no waits inside the rounds.
-template <int U, int J>
+template <int U, int J, bool WK>
 __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (&h)[5],
                                               const uint32_t (&Wc)[80], uint32_t (&Wn)[80],
                                               const uint8_t* ring, int lane) {
-    // block k+1 = unit m', sub-block j'; barrier when it opens a new unit
+    // Block k+1 (k = k0 + J, k0 a multiple of 2U) is unit (k0/U + (J+1)/U),
+    // whose parity is that of (J+1)/U since k0/U is even, and sub-block
+    // (J+1) % U: the slot address is a compile-time offset.  A barrier goes
+    // in front of the first read of every new unit.
     constexpr int jn = (J + 1) % U;
-    const uint32_t mn = (k + 1) / U;
-    const uint8_t* slot = ring + ((mn & 1u) * U + jn) * kWBlockBytes + lane * 16;
+    constexpr int slot_idx = (((J + 1) / U) & 1) * U + jn;
+    const uint8_t* slot = ring + slot_idx * kWBlockBytes + lane * 16;
     if constexpr (jn == 0) split_barrier();
     uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
     read_w_group<0>(slot, Wn);
     __builtin_amdgcn_sched_barrier(0);
-    RoundsW<0, 20>::run(v, Wc);
+    RoundsW<0, 20, WK>::run(v, Wc);
     __builtin_amdgcn_sched_barrier(0);
     read_w_group<1>(slot, Wn);
     __builtin_amdgcn_sched_barrier(0);
-    RoundsW<20, 40>::run(v, Wc);
+    RoundsW<20, 40, WK>::run(v, Wc);
     __builtin_amdgcn_sched_barrier(0);
     read_w_group<2>(slot, Wn);
     __builtin_amdgcn_sched_barrier(0);
-    RoundsW<40, 60>::run(v, Wc);
+    RoundsW<40, 60, WK>::run(v, Wc);
     __builtin_amdgcn_sched_barrier(0);
     read_w_group<3>(slot, Wn);
     __builtin_amdgcn_sched_barrier(0);
-    RoundsW<60, 80>::run(v, Wc);
+    RoundsW<60, 80, WK>::run(v, Wc);
     const bool live = k < T;
 #pragma unroll
     for (int i = 0; i < 5; ++i) h[i] = live ? h[i] + v[i] : h[i];
@@ -302,14 +308,14 @@ __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (
 
 // 2U blocks (two units) per consumer iteration, unrolled, so Wa/Wb keep
 // their parity and every barrier position is a compile-time constant.
-template <int U, int J>
+template <int U, int J, bool WK>
 struct ConsumeUnits {
     __device__ __forceinline__ static void run(uint32_t k0, uint32_t T, uint32_t (&h)[5],
                                                uint32_t (&Wa)[80], uint32_t (&Wb)[80],
                                                const uint8_t* ring, int lane) {
         if constexpr (J < 2 * U) {
-            consume_block<U, J>(k0 + J, T, h, Wa, Wb, ring, lane);
-            ConsumeUnits<U, J + 1>::run(k0, T, h, Wb, Wa, ring, lane);
+            consume_block<U, J, WK>(k0 + J, T, h, Wa, Wb, ring, lane);
+            ConsumeUnits<U, J + 1, WK>::run(k0, T, h, Wb, Wa, ring, lane);
         }
     }
 };
@@ -320,7 +326,7 @@ struct ConsumeUnits {
 // SIMD hosts exactly one consumer and its own producer (the consumer keeps
 // the SIMD's issue slots it needs; the producer fills the rest).  All waves
 // share one s_barrier sequence, so the unit count is the workgroup maximum.
-template <int U, int PAIRS>
+template <int U, int PAIRS, bool WK = true>
 __global__ __launch_bounds__(128 * PAIRS) void sha1_split_kernel(BatchArgs A) {
     static_assert(PAIRS * 2 * U * kWBlockBytes <= 160 * 1024, "LDS");
     __shared__ __attribute__((aligned(16))) uint8_t lds[PAIRS * 2 * U * kWBlockBytes];
@@ -366,14 +372,14 @@ __global__ __launch_bounds__(128 * PAIRS) void sha1_split_kernel(BatchArgs A) {
         if (S > 1) load_stage(en.p + 128, A1);
         uint32_t s = 0;
         for (; s + 1 < S; s += 2) {
-            produce_stage<U>(en, s, S, A0, ring, lane);
-            produce_stage<U>(en, s + 1, S, A1, ring, lane);
+            produce_stage<U, WK>(en, s, S, A0, ring, lane);
+            produce_stage<U, WK>(en, s + 1, S, A1, ring, lane);
         }
-        if (s < S) produce_stage<U>(en, s, S, A0, ring, lane);
+        if (s < S) produce_stage<U, WK>(en, s, S, A0, ring, lane);
         for (uint32_t k = 2 * S; k < units * U; ++k) {
             uint32_t w[16];
             if (k < T) tail_block_words(en, k, w);
-            produce_block<U>(k, w, ring, lane);
+            produce_block<U, WK>(k, w, ring, lane);
         }
         split_barrier();  // matches the consumer's last (unused) read
     } else {
@@ -387,7 +393,7 @@ __global__ __launch_bounds__(128 * PAIRS) void sha1_split_kernel(BatchArgs A) {
         read_w_group<2>(ring + lane * 16, Wa);
         read_w_group<3>(ring + lane * 16, Wa);
         for (uint32_t k = 0; k < units * U; k += 2 * U) {
-            ConsumeUnits<U, 0>::run(k, T, h, Wa, Wb, ring, lane);
+            ConsumeUnits<U, 0, WK>::run(k, T, h, Wa, Wb, ring, lane);
         }
         if (valid) emit(A, en.id, h);
     }
@@ -498,6 +504,8 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     case 1: hipLaunchKernelGGL((sha1_split_kernel<1, 1>), dim3(groups), dim3(128), 0, st, A); break;
     case 2: hipLaunchKernelGGL((sha1_split_kernel<2, 1>), dim3(groups), dim3(128), 0, st, A); break;
     case 3: hipLaunchKernelGGL((sha1_split_kernel<3, 1>), dim3(groups), dim3(128), 0, st, A); break;
+    case 6: hipLaunchKernelGGL((sha1_split_kernel<3, 1, false>), dim3(groups), dim3(128), 0, st, A); break;
+    case 7: hipLaunchKernelGGL((sha1_split_kernel<2, 1, false>), dim3(groups), dim3(128), 0, st, A); break;
     case 4:  // 4 pairs per workgroup (512 threads), one consumer + producer per SIMD
         hipLaunchKernelGGL((sha1_split_kernel<1, 4>), dim3((groups + 3) / 4), dim3(512), 0, st, A);
         break;

@@ -15,6 +15,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <mutex>
 #include <numeric>
 #include <string>
@@ -189,7 +190,7 @@ int choose_kernel(int kernel, size_t n, int cus) {
 int split_unit(size_t n, int cus) {
     if (const char* e = getenv("SHA1CHUNK_SPLIT_UNIT")) {
         const int u = atoi(e);
-        if (u >= 1 && u <= 5) return u;
+        if (u >= 1 && u <= 7) return u;
     }
     const size_t groups = (n + 63) / 64;
     if (groups <= size_t(cus)) return 3;
@@ -692,6 +693,198 @@ int sha1chunk_synth_fill_ragged_async(void* d_base, const uint64_t* d_offsets,
                                 count, seed, static_cast<hipStream_t>(stream));
     if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "synth launch: %s", hipGetErrorString(e));
     return SHA1CHUNK_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------ verify queue --
+// Two fill/flight sets per queue: while one set's batch is hashed and
+// compared on the device, submissions fill the other.  Set layout (pinned
+// host and device alike): [off u64 x B][len u32 x B][expected 20 x B] pad to
+// 128 | B slots of `stride` bytes; the device side adds B x 20 digests and
+// B mismatch bytes.
+namespace {
+struct VqSet {
+    PinBuf h;
+    DevBuf d;
+    PinBuf res;
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    std::vector<uint64_t> tags;
+    size_t count = 0;
+    bool inflight = false;
+};
+}  // namespace
+
+struct sha1chunk_vq {
+    int dev = 0;
+    int cus = 256;
+    size_t batch = 0;
+    uint32_t maxlen = 0;
+    size_t stride = 0, meta = 0;
+    VqSet set[2];
+    int fill = 0;
+    std::deque<int> flight;  // launched sets, oldest first
+    std::deque<std::pair<uint64_t, uint8_t>> ready;
+    size_t pending = 0;
+};
+
+namespace {
+
+uint64_t* vq_off(sha1chunk_vq* q, uint8_t* base) { return reinterpret_cast<uint64_t*>(base); }
+uint32_t* vq_len(sha1chunk_vq* q, uint8_t* base) {
+    return reinterpret_cast<uint32_t*>(base + q->batch * 8);
+}
+uint8_t* vq_exp(sha1chunk_vq* q, uint8_t* base) { return base + q->batch * 12; }
+
+int vq_launch(sha1chunk_vq* q, int which) {
+    VqSet& S = q->set[which];
+    if (S.count == 0) return SHA1CHUNK_OK;
+    HIP_TRY(hipSetDevice(q->dev));
+    uint8_t* h = static_cast<uint8_t*>(S.h.p);
+    uint8_t* d = static_cast<uint8_t*>(S.d.p);
+    HIP_TRY(hipMemcpyAsync(d, h, q->meta + S.count * q->stride, hipMemcpyHostToDevice, S.stream));
+    uint8_t* ddig = d + q->meta + q->batch * q->stride;
+    uint8_t* dmis = ddig + q->batch * 20;
+    BatchArgs A{};
+    A.base = d;
+    A.off = vq_off(q, d);
+    A.len = vq_len(q, d);
+    A.n = static_cast<uint32_t>(S.count);
+    A.dig = ddig;
+    int rc = launch_checked(choose_kernel(SHA1CHUNK_KERNEL_AUTO, S.count, q->cus), A, S.stream, q->cus);
+    if (rc) return rc;
+    hipError_t e = launch_compare(ddig, vq_exp(q, d), static_cast<uint32_t>(S.count), dmis, S.stream);
+    if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "compare launch: %s", hipGetErrorString(e));
+    HIP_TRY(hipMemcpyAsync(S.res.p, dmis, S.count, hipMemcpyDeviceToHost, S.stream));
+    HIP_TRY(hipEventRecord(S.done, S.stream));
+    S.inflight = true;
+    q->flight.push_back(which);
+    return SHA1CHUNK_OK;
+}
+
+// Move the oldest launched set's results to `ready` (blocking on it).
+int vq_collect_oldest(sha1chunk_vq* q) {
+    if (q->flight.empty()) return SHA1CHUNK_OK;
+    const int which = q->flight.front();
+    VqSet& S = q->set[which];
+    HIP_TRY(hipEventSynchronize(S.done));
+    const uint8_t* r = static_cast<const uint8_t*>(S.res.p);
+    for (size_t i = 0; i < S.count; ++i) q->ready.emplace_back(S.tags[i], r[i]);
+    S.tags.clear();
+    S.count = 0;
+    S.inflight = false;
+    q->flight.pop_front();
+    return SHA1CHUNK_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+sha1chunk_vq* sha1chunk_vq_create(size_t batch, uint32_t max_chunk_len) {
+    if (batch == 0 || batch > (1u << 20) || max_chunk_len == 0) {
+        fail(SHA1CHUNK_EINVAL, "vq: batch 1..2^20 and max_chunk_len > 0 required");
+        return nullptr;
+    }
+    Device* D;
+    if (get_device(&D)) return nullptr;
+    auto* q = new sha1chunk_vq();
+    q->dev = D->id;
+    q->cus = D->cus;
+    q->batch = batch;
+    q->maxlen = max_chunk_len;
+    q->stride = round_up(max_chunk_len, kAlign);
+    q->meta = round_up(batch * (8 + 4 + 20), kAlign);
+    const size_t hbytes = q->meta + batch * q->stride;
+    for (auto& S : q->set) {
+        if (S.h.ensure(hbytes) || S.d.ensure(hbytes + batch * 21) || S.res.ensure(batch) ||
+            hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&S.done, hipEventDisableTiming) != hipSuccess) {
+            if (t_err.empty()) fail(SHA1CHUNK_ENOMEM, "vq: allocation failed");
+            sha1chunk_vq_destroy(q);
+            return nullptr;
+        }
+        S.tags.reserve(batch);
+    }
+    return q;
+}
+
+int sha1chunk_vq_submit(sha1chunk_vq* q, const void* chunk, uint32_t len, const uint8_t expected[20],
+                        uint64_t tag) {
+    if (!q || (len && !chunk) || !expected) return fail(SHA1CHUNK_EINVAL, "vq: null argument");
+    if (len > q->maxlen) return fail(SHA1CHUNK_EINVAL, "vq: chunk of %u bytes > max %u", len, q->maxlen);
+    VqSet* S = &q->set[q->fill];
+    while (S->inflight) {  // the fill set is still on the device: drain in order
+        int rc = vq_collect_oldest(q);
+        if (rc) return rc;
+    }
+    uint8_t* h = static_cast<uint8_t*>(S->h.p);
+    const size_t i = S->count;
+    vq_off(q, h)[i] = q->meta + i * q->stride;
+    vq_len(q, h)[i] = len;
+    memcpy(vq_exp(q, h) + 20 * i, expected, 20);
+    if (len) memcpy(h + q->meta + i * q->stride, chunk, len);
+    S->tags.push_back(tag);
+    ++S->count;
+    ++q->pending;
+    if (S->count == q->batch) {
+        int rc = vq_launch(q, q->fill);
+        if (rc) return rc;
+        q->fill ^= 1;
+    }
+    return SHA1CHUNK_OK;
+}
+
+int sha1chunk_vq_flush(sha1chunk_vq* q) {
+    if (!q) return fail(SHA1CHUNK_EINVAL, "vq: null queue");
+    if (q->set[q->fill].count == 0 || q->set[q->fill].inflight) return SHA1CHUNK_OK;
+    int rc = vq_launch(q, q->fill);
+    if (rc) return rc;
+    q->fill ^= 1;
+    return SHA1CHUNK_OK;
+}
+
+long sha1chunk_vq_poll(sha1chunk_vq* q, uint64_t* tags, uint8_t* mismatch, size_t max, int wait) {
+    if (!q || (max && (!tags || !mismatch))) return fail(SHA1CHUNK_EINVAL, "vq: null argument");
+    int rc;
+    if (wait) {
+        if ((rc = sha1chunk_vq_flush(q))) return rc;
+        while (!q->flight.empty())
+            if ((rc = vq_collect_oldest(q))) return rc;
+    } else {
+        while (!q->flight.empty()) {
+            hipError_t e = hipEventQuery(q->set[q->flight.front()].done);
+            if (e == hipErrorNotReady) break;
+            if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "vq: %s", hipGetErrorString(e));
+            if ((rc = vq_collect_oldest(q))) return rc;
+        }
+    }
+    size_t n = 0;
+    while (n < max && !q->ready.empty()) {
+        tags[n] = q->ready.front().first;
+        mismatch[n] = q->ready.front().second;
+        q->ready.pop_front();
+        ++n;
+    }
+    q->pending -= n;
+    return static_cast<long>(n);
+}
+
+size_t sha1chunk_vq_pending(const sha1chunk_vq* q) { return q ? q->pending : 0; }
+
+void sha1chunk_vq_destroy(sha1chunk_vq* q) {
+    if (!q) return;
+    (void)hipSetDevice(q->dev);
+    for (auto& S : q->set) {
+        if (S.stream) (void)hipStreamSynchronize(S.stream);
+        if (S.done) (void)hipEventDestroy(S.done);
+        if (S.stream) (void)hipStreamDestroy(S.stream);
+        if (S.h.p) (void)hipHostFree(S.h.p);
+        if (S.res.p) (void)hipHostFree(S.res.p);
+        if (S.d.p) (void)hipFree(S.d.p);
+    }
+    delete q;
 }
 
 }  // extern "C"

@@ -85,6 +85,12 @@ _SIGNATURES = [
     ("sha1chunk_finish", C.c_int, [_u32p, C.c_uint64, _vp, C.c_uint32, _u8p]),
     ("sha1chunk_synth_fill_async", C.c_int, [_vp, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint64, _vp]),
     ("sha1chunk_synth_fill_ragged_async", C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64, _vp]),
+    ("sha1chunk_vq_create", C.c_void_p, [C.c_size_t, C.c_uint32]),
+    ("sha1chunk_vq_submit", C.c_int, [_vp, _vp, C.c_uint32, _u8p, C.c_uint64]),
+    ("sha1chunk_vq_flush", C.c_int, [_vp]),
+    ("sha1chunk_vq_poll", C.c_long, [_vp, _u64p, _u8p, C.c_size_t, C.c_int]),
+    ("sha1chunk_vq_pending", C.c_size_t, [_vp]),
+    ("sha1chunk_vq_destroy", None, [_vp]),
     ("sha1chunk_device_count", C.c_int, []),
     ("sha1chunk_set_device", C.c_int, [C.c_int]),
     ("sha1chunk_get_device", C.c_int, []),
@@ -261,6 +267,58 @@ def verify_batch(base, offsets, lengths, expected: np.ndarray) -> np.ndarray:
                                         off.size, _np_ptr(exp), _np_ptr(mism), HOST),
            "sha1chunk_verify_batch")
     return mism
+
+
+class VerifyQueue:
+    """Asynchronous batched verify for the peer's receive path: the batched
+    counterpart of verify_hash() (job.c:217-228).  submit() stages a chunk
+    with its expected digest and a tag; poll() yields (tag, mismatch) with
+    mismatch 0 = match, 1 = mismatch (re-GET), as verify_hash returns."""
+
+    def __init__(self, batch: int = 256, max_chunk_len: int = CHUNK_LEN):
+        self._q = lib().sha1chunk_vq_create(batch, max_chunk_len)
+        if not self._q:
+            raise Sha1ChunkError(ENODEV if device_count() == 0 else EINVAL, "sha1chunk_vq_create",
+                                 lib().sha1chunk_last_error().decode(errors="replace"))
+
+    def submit(self, chunk: bytes, expected: bytes | str, tag: int) -> None:
+        exp = bytes.fromhex(expected) if isinstance(expected, str) else bytes(expected)
+        if len(exp) != DIGEST_LEN:
+            raise ValueError("expected digest must be 20 bytes / 40 hex chars")
+        e = np.frombuffer(exp, np.uint8)
+        b = bytes(chunk)
+        _check(lib().sha1chunk_vq_submit(self._q, b, len(b), _np_ptr(e), tag), "sha1chunk_vq_submit")
+
+    def flush(self) -> None:
+        _check(lib().sha1chunk_vq_flush(self._q), "sha1chunk_vq_flush")
+
+    def poll(self, wait: bool = False, max_results: int = 1 << 16) -> list[tuple[int, int]]:
+        tags = np.zeros(max_results, np.uint64)
+        mism = np.zeros(max_results, np.uint8)
+        n = _check(lib().sha1chunk_vq_poll(self._q, _np_ptr(tags, _u64p), _np_ptr(mism), max_results,
+                                           1 if wait else 0), "sha1chunk_vq_poll")
+        return [(int(tags[i]), int(mism[i])) for i in range(n)]
+
+    @property
+    def pending(self) -> int:
+        return int(lib().sha1chunk_vq_pending(self._q))
+
+    def close(self) -> None:
+        if self._q:
+            lib().sha1chunk_vq_destroy(self._q)
+            self._q = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 # ------------------------------------------------------ device (torch) ----

@@ -110,6 +110,28 @@ int sha1chunk_synth_fill_ragged_async(void *d_base, const uint64_t *d_offsets,
                                       const uint32_t *d_lengths, uint64_t first, uint64_t count,
                                       uint64_t seed, void *stream);
 
+/* ---- Asynchronous verify queue (the peer's receive path) --
+ * The reference verifies each reassembled chunk synchronously inside its
+ * select() loop (packet_handler.c:469-472 -> job.c:217 verify_hash).  A queue
+ * batches them instead: submit() copies the chunk into pinned staging (the
+ * caller may reuse its buffer at once) with its expected digest and a tag;
+ * every `batch` submissions (or on flush) the batch is hashed and compared on
+ * the device asynchronously; poll() returns finished (tag, mismatch) pairs,
+ * mismatch following verify_hash: 0 = match, 1 = mismatch -> re-GET.  One
+ * queue per thread; queues on one device share nothing. */
+typedef struct sha1chunk_vq sha1chunk_vq;
+/* NULL on failure (sha1chunk_last_error() says why). */
+sha1chunk_vq *sha1chunk_vq_create(size_t batch, uint32_t max_chunk_len);
+int sha1chunk_vq_submit(sha1chunk_vq *q, const void *chunk, uint32_t len,
+                        const uint8_t expected[20], uint64_t tag);
+int sha1chunk_vq_flush(sha1chunk_vq *q);
+/* Up to max finished results; wait != 0 blocks until everything submitted so
+ * far has finished.  Returns the number written (>= 0) or a negative error. */
+long sha1chunk_vq_poll(sha1chunk_vq *q, uint64_t *tags, uint8_t *mismatch, size_t max, int wait);
+/* Submitted but not yet returned by poll(). */
+size_t sha1chunk_vq_pending(const sha1chunk_vq *q);
+void sha1chunk_vq_destroy(sha1chunk_vq *q);
+
 /* Device management. */
 int sha1chunk_device_count(void);
 int sha1chunk_set_device(int device);

@@ -114,6 +114,13 @@ def test_no_device_fails_loudly(pkg, built):
     assert r.stdout == ""
 
 
+def test_verify_queue_without_device_fails_loudly(pkg):
+    if _has_device(pkg):
+        pytest.skip("a device is present")
+    with pytest.raises(pkg.Sha1ChunkError):
+        pkg.VerifyQueue(batch=16)
+
+
 def test_python_mirror_names(pkg):
     for name in ("shahash", "binary2hex", "hex2binary", "make_chunks", "get_chunk_hash",
                  "verify_hash", "SHA1"):

@@ -295,3 +295,38 @@ def test_host_batch_all_devices(pkg, dev, oracle, golden):
     got = pkg.hash_batch(host, off, np.full(n, L512, np.uint32), all_devices=True)
     want = np.fromfile(os.path.join(GOLDEN, "synth_4096x512k.bin"), np.uint8).reshape(-1, 20)[:n]
     assert np.array_equal(got, want)
+
+
+# ------------------------------------------------------- verify queue ----
+def test_verify_queue_receive_path(pkg, dev, oracle, golden, fixture_files):
+    """Batched async verify (packet_handler.c:469-472 -> job.c:217): every
+    result comes back exactly once with verify_hash's 0/1 convention."""
+    rng = np.random.default_rng(77)
+    chunks, expected, want = [], [], {}
+    ctar = fixture_files["tmp/C.tar"]
+    for i in range(4):  # the reference's own fixture chunks
+        chunks.append(ctar[i * L512:(i + 1) * L512])
+        expected.append(golden["fixtures"]["C.chunks_file"][i])
+    lens = oracle.mixed_lengths(150)
+    for i in range(150):  # ragged, smaller-than-chunk payloads too
+        d = oracle.synth_chunk(i, int(min(lens[i], L512))).tobytes()
+        chunks.append(d)
+        expected.append(oracle.shahash(d).hex())
+    for t, (c, e) in enumerate(zip(chunks, expected)):
+        bad = rng.random() < 0.2
+        if bad:
+            e = ("0" if e[0] != "0" else "1") + e[1:]
+        want[1000 + t] = 1 if bad else 0
+    got = {}
+    with pkg.VerifyQueue(batch=32, max_chunk_len=L512) as q:
+        for t, (c, e) in enumerate(zip(chunks, expected)):
+            e2 = e if want[1000 + t] == 0 else ("0" if e[0] != "0" else "1") + e[1:]
+            q.submit(c, e2, 1000 + t)
+            for tag, m in q.poll():
+                assert tag not in got
+                got[tag] = m
+        for tag, m in q.poll(wait=True):
+            assert tag not in got
+            got[tag] = m
+        assert q.pending == 0
+    assert got == want
