@@ -330,3 +330,89 @@ def test_verify_queue_receive_path(pkg, dev, oracle, golden, fixture_files):
             got[tag] = m
         assert q.pending == 0
     assert got == want
+
+
+# ------------------------------------- sender verify + master index ----
+_VERIFY_DRIVER = r'''
+#include <stdio.h>
+#include <stdlib.h>
+#include "chunk_hash.h"
+/* argv: file idx hex [idx hex ...] -> verify_chunk_hash each pair in order */
+int main(int argc, char **argv) {
+    FILE *f = fopen(argv[1], "r");
+    if (!f) return 2;
+    for (int i = 2; i + 1 < argc; i += 2) {
+        verify_chunk_hash(f, argv[i + 1], (size_t)atoll(argv[i]));
+        printf("ok %s pos %ld\n", argv[i], ftell(f));
+    }
+    fclose(f);
+    return 0;
+}
+'''
+
+
+@pytest.fixture(scope="module")
+def verify_driver(tmp_path_factory):
+    d = tmp_path_factory.mktemp("vdrv")
+    src = d / "vdrv.c"
+    src.write_text(_VERIFY_DRIVER)
+    exe = d / "vdrv"
+    subprocess.run(["gcc", "-O1", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
+                    "-L", PKG_DIR, "-lsha1chunk", f"-Wl,-rpath,{PKG_DIR}"], check=True)
+    return str(exe)
+
+
+def _run_verify(exe, path, pairs, index=True):
+    env = dict(os.environ, SHA1CHUNK_MASTER_INDEX="1" if index else "0")
+    args = [exe, path] + [x for i, h in pairs for x in (str(i), h)]
+    return subprocess.run(args, capture_output=True, text=True, env=env)
+
+
+def test_verify_chunk_hash_master_index(pkg, dev, golden, fixture_files, verify_driver, tmp_path):
+    """chunk.c:204-217 as the sender calls it per GET (packet_handler.c:434):
+    the C.tar fixture chunks, repeated so the master-file index serves the
+    later calls; stdout and the stream position match the per-call path."""
+    import hashlib
+    p = tmp_path / "C.tar"
+    p.write_bytes(fixture_files["tmp/C.tar"])
+    want = golden["fixtures"]["C.chunks_file"]
+    pairs = [(i, want[i]) for i in (0, 3, 1, 2, 2, 0, 3)]
+    # a request past EOF hashes a zero chunk (calloc'd buffer, nothing read)
+    pairs.append((5, hashlib.sha1(bytes(L512)).hexdigest()))
+    a = _run_verify(verify_driver, str(p), pairs, index=True)
+    b = _run_verify(verify_driver, str(p), pairs, index=False)
+    assert a.returncode == 0, a.stderr
+    assert b.returncode == 0, b.stderr
+    assert a.stdout == b.stdout
+    assert a.stdout.count("the ascii of calculated hash is") == len(pairs)
+
+
+def test_verify_chunk_hash_ragged_master_and_mismatch(pkg, dev, oracle, verify_driver, tmp_path):
+    """A master file whose last chunk is short: the verify hashes it zero-
+    padded to CHUNK_LEN (both paths); a wrong hash served from the index
+    still exits(-1) with the reference's message."""
+    import hashlib
+    size = 3 * L512 + 123457
+    data = oracle.synth_chunks(900, 4, L512).tobytes()[:size]
+    p = tmp_path / "master.dat"
+    p.write_bytes(data)
+    padded = data + bytes(4 * L512 - size)
+    hexes = [hashlib.sha1(padded[i * L512:(i + 1) * L512]).hexdigest() for i in range(4)]
+    pairs = [(3, hexes[3]), (0, hexes[0]), (3, hexes[3]), (2, hexes[2]), (1, hexes[1])]
+    a = _run_verify(verify_driver, str(p), pairs, index=True)
+    b = _run_verify(verify_driver, str(p), pairs, index=False)
+    assert a.returncode == 0 and b.returncode == 0, (a.stderr, b.stderr)
+    assert a.stdout == b.stdout
+    bad = hexes[1][:-1] + ("0" if hexes[1][-1] != "0" else "1")
+    c = _run_verify(verify_driver, str(p), [(0, hexes[0]), (2, hexes[2]), (1, bad)], index=True)
+    assert c.returncode == 255
+    assert "Unmatched chunk hashes" in c.stderr and hexes[1] in c.stderr
+    assert c.stdout.count("ok ") == 2
+    # the file changes under the peer: the index is rebuilt, not reused
+    data2 = bytearray(data)
+    data2[L512 + 5] ^= 0xFF
+    p.write_bytes(bytes(data2))
+    os.utime(p, ns=(1, 1))
+    new1 = hashlib.sha1(bytes(data2[L512:2 * L512])).hexdigest()
+    d = _run_verify(verify_driver, str(p), [(1, new1), (1, new1), (0, hexes[0])], index=True)
+    assert d.returncode == 0, d.stderr

@@ -24,9 +24,12 @@ def main():
     ap.add_argument("--kernels", default="lane,fused,split")
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--lib", default=None, help="A/B: load this libsha1chunk.so instead")
     a = ap.parse_args()
     import torch
     pkg = importlib.import_module("congestion-control-with-bittorren_amd")
+    if a.lib:
+        pkg.sha1chunk.LIB_PATH = os.path.abspath(a.lib)
     torch.cuda.set_device(0)
     pkg.set_device(0)
     L = a.chunk_len

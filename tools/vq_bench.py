@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""Throughput of the receive-path verify queue (sha1chunk_vq_*, SURVEY 8f
+rank 2): a peer that reassembled N 512 KiB chunks in host memory submits
+each with its expected digest and drains 0/1 results, as packet_handler.c:472
+-> job.c:217 would.  Expected digests come from hashlib (stdlib) so this tool
+needs nothing from oracle/.  Reports chunks/s and GiB/s end-to-end (host
+bytes -> pinned staging -> H2D -> kernel -> compare -> D2H -> results)."""
+from __future__ import annotations
+
+import argparse
+import hashlib
+import importlib
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--chunks", type=int, default=4096)
+    ap.add_argument("--distinct", type=int, default=256, help="distinct host buffers reused round-robin")
+    ap.add_argument("--batches", default="64,256,1024")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    pkg = importlib.import_module("congestion-control-with-bittorren_amd")
+    L = pkg.sha1chunk.CHUNK_LEN
+    rng = np.random.default_rng(5)
+    bufs = [rng.integers(0, 256, L, dtype=np.uint8).tobytes() for _ in range(a.distinct)]
+    digs = [hashlib.sha1(b).digest() for b in bufs]
+    bad = set(range(3, a.chunks, 97))
+    rows = []
+    for batch in [int(x) for x in a.batches.split(",")]:
+        with pkg.VerifyQueue(batch=batch, max_chunk_len=L) as q:
+            # warm-up batch
+            for i in range(batch):
+                q.submit(bufs[i % a.distinct], digs[i % a.distinct], i)
+            q.poll(wait=True)
+            t0 = time.perf_counter()
+            got = {}
+            for i in range(a.chunks):
+                d = digs[i % a.distinct]
+                if i in bad:
+                    d = bytes([d[0] ^ 1]) + d[1:]
+                q.submit(bufs[i % a.distinct], d, i)
+                if (i & 63) == 63:
+                    got.update(q.poll())
+            got.update(q.poll(wait=True))
+            dt = time.perf_counter() - t0
+        ok = len(got) == a.chunks and all(got[i] == (1 if i in bad else 0) for i in range(a.chunks))
+        row = {"batch": batch, "chunks": a.chunks, "seconds": round(dt, 4),
+               "chunks_per_s": round(a.chunks / dt, 1), "GiBps": round(a.chunks * L / dt / 2**30, 3),
+               "results_correct": ok}
+        print(json.dumps(row), flush=True)
+        rows.append(row)
+        if not ok:
+            sys.exit(1)
+    if a.out:
+        json.dump(rows, open(a.out, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
