@@ -273,7 +273,7 @@ __device__ __forceinline__ void read_w_group(const uint8_t* slot, uint32_t (&W)[
 // Consumer: rounds of block k from Wc while W(k+1) streams into Wn.  All of
 // it is straight-line (the barrier position is a compile-time function of
 // the unrolled block index), so hipcc inserts no waits inside the rounds.
-template <int U, int J, bool WK>
+template <int U, int J, bool WK, bool MASK>
 __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (&h)[5],
                                               const uint32_t (&Wc)[80], uint32_t (&Wn)[80],
                                               const uint8_t* ring, int lane) {
@@ -301,21 +301,26 @@ __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (
     read_w_group<3>(slot, Wn);
     __builtin_amdgcn_sched_barrier(0);
     RoundsW<60, 80, WK>::run(v, Wc);
-    const bool live = k < T;
+    if constexpr (MASK) {
+        const bool live = k < T;
 #pragma unroll
-    for (int i = 0; i < 5; ++i) h[i] = live ? h[i] + v[i] : h[i];
+        for (int i = 0; i < 5; ++i) h[i] = live ? h[i] + v[i] : h[i];
+    } else {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) h[i] += v[i];
+    }
 }
 
 // 2U blocks (two units) per consumer iteration, unrolled, so Wa/Wb keep
 // their parity and every barrier position is a compile-time constant.
-template <int U, int J, bool WK>
+template <int U, int J, bool WK, bool MASK>
 struct ConsumeUnits {
     __device__ __forceinline__ static void run(uint32_t k0, uint32_t T, uint32_t (&h)[5],
                                                uint32_t (&Wa)[80], uint32_t (&Wb)[80],
                                                const uint8_t* ring, int lane) {
         if constexpr (J < 2 * U) {
-            consume_block<U, J, WK>(k0 + J, T, h, Wa, Wb, ring, lane);
-            ConsumeUnits<U, J + 1, WK>::run(k0, T, h, Wb, Wa, ring, lane);
+            consume_block<U, J, WK, MASK>(k0 + J, T, h, Wa, Wb, ring, lane);
+            ConsumeUnits<U, J + 1, WK, MASK>::run(k0, T, h, Wb, Wa, ring, lane);
         }
     }
 };
@@ -392,8 +397,16 @@ __global__ __launch_bounds__(128 * PAIRS) void sha1_split_kernel(BatchArgs A) {
         read_w_group<1>(ring + lane * 16, Wa);
         read_w_group<2>(ring + lane * 16, Wa);
         read_w_group<3>(ring + lane * 16, Wa);
-        for (uint32_t k = 0; k < units * U; k += 2 * U) {
-            ConsumeUnits<U, 0, WK>::run(k, T, h, Wa, Wb, ring, lane);
+        // Iterations in which every valid lane is still inside its chunk
+        // commit without the per-lane select (all of them for equal lengths).
+        const uint32_t Tmin = __builtin_amdgcn_readfirstlane(wave_min(valid ? T : 0xffffffffu));
+        const uint32_t full = min(Tmin, units * U) / (2 * U) * (2 * U);
+        uint32_t k = 0;
+        for (; k < full; k += 2 * U) {
+            ConsumeUnits<U, 0, WK, false>::run(k, T, h, Wa, Wb, ring, lane);
+        }
+        for (; k < units * U; k += 2 * U) {
+            ConsumeUnits<U, 0, WK, true>::run(k, T, h, Wa, Wb, ring, lane);
         }
         if (valid) emit(A, en.id, h);
     }
