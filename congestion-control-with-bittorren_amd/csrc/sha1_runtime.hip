@@ -95,6 +95,7 @@ struct Slot {
     DevBuf ddig;
     hipStream_t stream = nullptr;
     hipEvent_t done = nullptr;
+    hipEvent_t copied = nullptr;  // this slot's H2D has landed (copy stream)
     bool busy = false;
     // bookkeeping for the batch in flight
     std::vector<uint32_t> ids;  // caller chunk index of each staged entry
@@ -106,6 +107,11 @@ struct Device {
     int id = -1;
     int cus = 256;
     Slot slot[2];
+    // Every slot's H2D goes through this one stream: copies run back to back
+    // at the full PCIe rate instead of two slots splitting it (which would
+    // delay the first kernel), and the next slot's copy queues behind the
+    // current one while the current slot's kernel runs.
+    hipStream_t copy = nullptr;
     DevBuf small;  // streaming calls: state + data
     PinBuf small_pin;
 };
@@ -162,7 +168,9 @@ int get_device(Device** out) {
             for (auto& s : D.slot) {
                 HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
                 HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+                HIP_TRY(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
             }
+            HIP_TRY(hipStreamCreateWithFlags(&D.copy, hipStreamNonBlocking));
             D.ready = true;
         }
     }
@@ -232,6 +240,13 @@ size_t slot_bytes_for(uint64_t total) {
     return std::min(hi, std::max(lo, static_cast<size_t>(total / 4)));
 }
 
+// The slot's stream waits for its H2D copies, issued on the copy stream.
+int copies_issued(Device& D, Slot& s) {
+    HIP_TRY(hipEventRecord(s.copied, D.copy));
+    HIP_TRY(hipStreamWaitEvent(s.stream, s.copied, 0));
+    return SHA1CHUNK_OK;
+}
+
 bool host_pinned(const void* p) {
     hipPointerAttribute_t at;
     if (hipPointerGetAttributes(&at, p) != hipSuccess) {
@@ -279,11 +294,12 @@ int stage_and_launch(Device& D, Slot& s, const uint8_t* base, const uint64_t* of
     }
     uint8_t* d = static_cast<uint8_t*>(s.dmem.p);
     if (direct) {
-        HIP_TRY(hipMemcpyAsync(d, h, meta, hipMemcpyHostToDevice, s.stream));
-        if (span) HIP_TRY(hipMemcpyAsync(d + meta, base + span0, span, hipMemcpyHostToDevice, s.stream));
+        HIP_TRY(hipMemcpyAsync(d, h, meta, hipMemcpyHostToDevice, D.copy));
+        if (span) HIP_TRY(hipMemcpyAsync(d + meta, base + span0, span, hipMemcpyHostToDevice, D.copy));
     } else {
-        HIP_TRY(hipMemcpyAsync(d, h, cur, hipMemcpyHostToDevice, s.stream));
+        HIP_TRY(hipMemcpyAsync(d, h, cur, hipMemcpyHostToDevice, D.copy));
     }
+    if ((rc = copies_issued(D, s))) return rc;
     BatchArgs A{};
     A.base = d;
     A.off = reinterpret_cast<const uint64_t*>(d);
@@ -559,7 +575,8 @@ long sha1chunk_hash_stream(sha1chunk_reader_fn reader, void* reader_ctx, sha1chu
             hlen[j] = static_cast<uint32_t>(
                 std::min<size_t>(SHA1CHUNK_CHUNK_LEN, got - j * SHA1CHUNK_CHUNK_LEN));
         }
-        HIP_TRY(hipMemcpyAsync(s.dmem.p, h, meta + got, hipMemcpyHostToDevice, s.stream));
+        HIP_TRY(hipMemcpyAsync(s.dmem.p, h, meta + got, hipMemcpyHostToDevice, D->copy));
+        if ((rc = copies_issued(*D, s))) return rc;
         uint8_t* d = static_cast<uint8_t*>(s.dmem.p);
         BatchArgs A{};
         A.base = d;

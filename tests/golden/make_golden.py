@@ -15,6 +15,7 @@ Outputs (small; committed):
   C.tar.gz                the reference's tmp/C.tar fixture (= A.tar || B.tar)
   synth_4096x512k.bin     all 4096 digests of BASELINE config 2
   mixed_16384.bin         all digests of BASELINE config 5 (mixed lengths)
+  mixed_16384_len.bin     its 16384 chunk lengths (uint32 LE)
 """
 from __future__ import annotations
 
@@ -179,6 +180,7 @@ def main() -> None:
         buf[int(off5[i]):int(off5[i]) + L] = O.synth_chunk(i, L)
     d5 = ref_digests(buf, off5, ln5)
     d5.tofile(os.path.join(OUT, "mixed_16384.bin"))
+    ln5.astype("<u4").tofile(os.path.join(OUT, "mixed_16384_len.bin"))
     g["config5"] = {"chunks": n5, "total_bytes": int(ln5.astype(np.uint64).sum()),
                     "agg": O.digest_of_digests(d5).hex(),
                     "lengths_sha1": hashlib.sha1(ln5.tobytes()).hexdigest()}
