@@ -146,6 +146,27 @@ static void hashes_sink(void *ctx, size_t first, const uint8_t *dig, size_t coun
 }
 
 int make_chunks(FILE *fp, uint8_t **chunk_hashes) {
+    /* Regular file: hash from the stream position to EOF through
+     * sha1chunk_hash_fd (multi-threaded pread into the pinned slots). */
+    struct stat st;
+    const int fd = fileno(fp);
+    const off_t pos = ftello(fp);
+    if (fd >= 0 && pos >= 0 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode)) {
+        const size_t cap = st.st_size > pos ? (size_t)((st.st_size - pos + CHUNK_LEN - 1) / CHUNK_LEN) : 0;
+        uint8_t *tmp = (uint8_t *)malloc(20 * (cap ? cap : 1));
+        if (!tmp) {
+            fprintf(stderr, "Failed to allocate memory\n");
+            exit(-1);
+        }
+        fseeko(fp, pos, SEEK_SET); /* drops stdio's read-ahead: fd offset = pos */
+        size_t total = 0;
+        long n = sha1chunk_hash_fd(fd, tmp, cap, &total);
+        if (n < 0) die("make_chunks", (int)n);
+        for (long i = 0; i < n; ++i) memcpy(chunk_hashes[i], tmp + 20 * i, 20);
+        free(tmp);
+        fseeko(fp, 0, SEEK_END); /* where the reference's fread loop leaves it */
+        return (int)n;
+    }
     long n = sha1chunk_hash_stream(file_reader, fp, hashes_sink, chunk_hashes);
     if (n < 0) die("make_chunks", (int)n);
     return (int)n;

@@ -416,3 +416,46 @@ def test_verify_chunk_hash_ragged_master_and_mismatch(pkg, dev, oracle, verify_d
     new1 = hashlib.sha1(bytes(data2[L512:2 * L512])).hexdigest()
     d = _run_verify(verify_driver, str(p), [(1, new1), (1, new1), (0, hexes[0])], index=True)
     assert d.returncode == 0, d.stderr
+
+
+_MAKE_CHUNKS_DRIVER = r'''
+#include <stdio.h>
+#include <stdlib.h>
+#include <stdint.h>
+#include "chunk_hash.h"
+/* argv: file skip_bytes -> make_chunks from the FILE* after fread(skip) */
+int main(int argc, char **argv) {
+    FILE *f = fopen(argv[1], "r");
+    size_t skip = (size_t)atoll(argv[2]);
+    char *tmp = malloc(skip + 1);
+    if (!f || fread(tmp, 1, skip, f) != skip) return 2;
+    uint8_t *store = malloc(20 * 64), *h[64];
+    for (int i = 0; i < 64; ++i) h[i] = store + 20 * i;
+    int n = make_chunks(f, h);
+    char hex[41];
+    for (int i = 0; i < n; ++i) { binary2hex(h[i], 20, hex); printf("%d %s\n", i, hex); }
+    printf("eof %d\n", fgetc(f) == EOF);
+    return 0;
+}
+'''
+
+
+def test_make_chunks_from_stream_position(pkg, dev, golden, fixture_files, tmp_path):
+    """chunk.c:15-27 hashes from the FILE*'s current position to EOF, even
+    after stdio has buffered ahead of it."""
+    src = tmp_path / "mc.c"
+    src.write_text(_MAKE_CHUNKS_DRIVER)
+    exe = tmp_path / "mc"
+    subprocess.run(["gcc", "-O1", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
+                    "-L", PKG_DIR, "-lsha1chunk", f"-Wl,-rpath,{PKG_DIR}"], check=True)
+    p = tmp_path / "C.tar"
+    p.write_bytes(fixture_files["tmp/C.tar"])
+    want = golden["fixtures"]["C.chunks_file"]
+    out = subprocess.run([str(exe), str(p), str(L512)], capture_output=True, text=True, check=True).stdout
+    assert out == "".join(f"{i} {h}\n" for i, h in enumerate(want[1:])) + "eof 1\n"
+    # an unaligned start: chunks are cut from the position, not the file start
+    import hashlib
+    data = fixture_files["tmp/C.tar"][1000:]
+    exp = [hashlib.sha1(data[i:i + L512]).hexdigest() for i in range(0, len(data), L512)]
+    out = subprocess.run([str(exe), str(p), "1000"], capture_output=True, text=True, check=True).stdout
+    assert out == "".join(f"{i} {h}\n" for i, h in enumerate(exp)) + "eof 1\n"

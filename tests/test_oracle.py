@@ -59,6 +59,8 @@ def test_mixed_prefix(oracle, golden):
                        np.uint8).reshape(-1, 20)
     ln = oracle.mixed_lengths(golden["config5"]["chunks"])
     assert hashlib.sha1(ln.tobytes()).hexdigest() == golden["config5"]["lengths_sha1"]
+    fixture = np.fromfile(os.path.join(os.path.dirname(__file__), "golden/mixed_16384_len.bin"), "<u4")
+    assert np.array_equal(fixture, ln)
     for i in list(range(48)) + [16383]:
         d = oracle.shahash(oracle.synth_chunk(i, int(ln[i])).tobytes())
         assert d == want[i].tobytes(), i
