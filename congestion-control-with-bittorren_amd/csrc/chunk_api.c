@@ -158,7 +158,12 @@ int make_chunks(FILE *fp, uint8_t **chunk_hashes) {
             fprintf(stderr, "Failed to allocate memory\n");
             exit(-1);
         }
-        fseeko(fp, pos, SEEK_SET); /* drops stdio's read-ahead: fd offset = pos */
+        /* stdio may have read ahead of `pos` (and a seek inside its buffer
+         * does not move the fd), so set the fd offset explicitly */
+        if (lseek(fd, pos, SEEK_SET) != pos) {
+            fprintf(stderr, "sha1chunk: make_chunks: lseek failed\n");
+            exit(-1);
+        }
         size_t total = 0;
         long n = sha1chunk_hash_fd(fd, tmp, cap, &total);
         if (n < 0) die("make_chunks", (int)n);
@@ -253,8 +258,9 @@ static int same_key(const file_key *a, const file_key *b) {
            a->mtime.tv_sec == b->mtime.tv_sec && a->mtime.tv_nsec == b->mtime.tv_nsec;
 }
 
-/* Copies chunk `idx`'s digest from the index into out20; 0 if unavailable. */
-static int master_lookup(FILE *f, size_t idx, uint8_t out20[20]) {
+/* Copies chunk `idx`'s digest from the index into out20 and the file size
+ * into *size; 0 if unavailable. */
+static int master_lookup(FILE *f, size_t idx, uint8_t out20[20], off_t *size) {
     const char *env = getenv("SHA1CHUNK_MASTER_INDEX");
     if (env && env[0] == '0') return 0;
     struct stat st;
@@ -287,6 +293,7 @@ static int master_lookup(FILE *f, size_t idx, uint8_t out20[20]) {
     }
     if (master.digest && idx < master.nchunks) {
         memcpy(out20, master.digest + 20 * idx, 20);
+        *size = st.st_size;
         hit = 1;
     }
     pthread_mutex_unlock(&master.mu);
@@ -299,7 +306,8 @@ void verify_chunk_hash(FILE *f, char *requested_chunk_hash, size_t chunk_idx) {
      * zero so the result is deterministic.  Offsets are 64-bit. */
     char *calculated;
     uint8_t hash[SHA1_HASH_SIZE];
-    if (master_lookup(f, chunk_idx, hash)) {
+    off_t size = 0;
+    if (master_lookup(f, chunk_idx, hash, &size)) {
         /* same observable behaviour as the per-call path: the two lines
          * get_chunk_hash prints, and the stream left after the chunk */
         calculated = (char *)malloc(SHA1_HASH_SIZE * 2 + 1);
@@ -310,7 +318,8 @@ void verify_chunk_hash(FILE *f, char *requested_chunk_hash, size_t chunk_idx) {
         fprintf(stdout, "calculating chunk hash for a chunk of size %d\n", CHUNK_LEN);
         hex2ascii(hash, SHA1_HASH_SIZE, calculated);
         fprintf(stdout, "the ascii of calculated hash is %s\n", calculated);
-        fseeko(f, (off_t)(chunk_idx + 1) * CHUNK_LEN, SEEK_SET);
+        const off_t after = (off_t)(chunk_idx + 1) * CHUNK_LEN; /* idx < nchunks: starts before EOF */
+        fseeko(f, after < size ? after : size, SEEK_SET);
     } else {
         fseeko(f, (off_t)chunk_idx * CHUNK_LEN, SEEK_SET);
         char *buffer = (char *)calloc(1, CHUNK_LEN);

@@ -273,7 +273,19 @@ __device__ __forceinline__ void read_w_group(const uint8_t* slot, uint32_t (&W)[
 // Consumer: rounds of block k from Wc while W(k+1) streams into Wn.  All of
 // it is straight-line (the barrier position is a compile-time function of
 // the unrolled block index), so hipcc inserts no waits inside the rounds.
-template <int U, int J, bool WK, bool MASK>
+// Split-kernel variant flags (A/B switches, defaults in kSplitV).
+constexpr int kVWK = 1;      // producer ships W+K (consumer: one VOP2 add)
+constexpr int kVRtSlot = 2;  // slot address computed at run time
+constexpr int kVUnmask = 4;  // unmasked commit while every lane is live
+// Measured on MI355X (profiles/split_variants_r01.json, 4096..32768
+// chunks): with 3-block units the W+K hand-off costs more on the producer
+// side than it saves in the consumer and the run-time slot address is
+// faster; with 2-block units W+K wins (by ~5%) and the slot form does not
+// matter.  Unmasked commit helps both.
+template <int U>
+constexpr int kSplitV = U == 3 ? (kVRtSlot | kVUnmask) : (kVWK | kVUnmask);
+
+template <int U, int J, int V, bool MASK>
 __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (&h)[5],
                                               const uint32_t (&Wc)[80], uint32_t (&Wn)[80],
                                               const uint8_t* ring, int lane) {
@@ -281,9 +293,16 @@ __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (
     // whose parity is that of (J+1)/U since k0/U is even, and sub-block
     // (J+1) % U: the slot address is a compile-time offset.  A barrier goes
     // in front of the first read of every new unit.
+    constexpr bool WK = (V & kVWK) != 0;
     constexpr int jn = (J + 1) % U;
     constexpr int slot_idx = (((J + 1) / U) & 1) * U + jn;
-    const uint8_t* slot = ring + slot_idx * kWBlockBytes + lane * 16;
+    const uint8_t* slot;
+    if constexpr ((V & kVRtSlot) != 0) {
+        const uint32_t mn = (k + 1) / U;
+        slot = ring + ((mn & 1u) * U + jn) * kWBlockBytes + lane * 16;
+    } else {
+        slot = ring + slot_idx * kWBlockBytes + lane * 16;
+    }
     if constexpr (jn == 0) split_barrier();
     uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
     read_w_group<0>(slot, Wn);
@@ -313,14 +332,14 @@ __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (
 
 // 2U blocks (two units) per consumer iteration, unrolled, so Wa/Wb keep
 // their parity and every barrier position is a compile-time constant.
-template <int U, int J, bool WK, bool MASK>
+template <int U, int J, int V, bool MASK>
 struct ConsumeUnits {
     __device__ __forceinline__ static void run(uint32_t k0, uint32_t T, uint32_t (&h)[5],
                                                uint32_t (&Wa)[80], uint32_t (&Wb)[80],
                                                const uint8_t* ring, int lane) {
         if constexpr (J < 2 * U) {
-            consume_block<U, J, WK, MASK>(k0 + J, T, h, Wa, Wb, ring, lane);
-            ConsumeUnits<U, J + 1, WK, MASK>::run(k0, T, h, Wb, Wa, ring, lane);
+            consume_block<U, J, V, MASK>(k0 + J, T, h, Wa, Wb, ring, lane);
+            ConsumeUnits<U, J + 1, V, MASK>::run(k0, T, h, Wb, Wa, ring, lane);
         }
     }
 };
@@ -331,8 +350,9 @@ struct ConsumeUnits {
 // SIMD hosts exactly one consumer and its own producer (the consumer keeps
 // the SIMD's issue slots it needs; the producer fills the rest).  All waves
 // share one s_barrier sequence, so the unit count is the workgroup maximum.
-template <int U, int PAIRS, bool WK = true>
+template <int U, int PAIRS, int V = kSplitV<U>>
 __global__ __launch_bounds__(128 * PAIRS) void sha1_split_kernel(BatchArgs A) {
+    constexpr bool WK = (V & kVWK) != 0;
     static_assert(PAIRS * 2 * U * kWBlockBytes <= 160 * 1024, "LDS");
     __shared__ __attribute__((aligned(16))) uint8_t lds[PAIRS * 2 * U * kWBlockBytes];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -400,13 +420,13 @@ __global__ __launch_bounds__(128 * PAIRS) void sha1_split_kernel(BatchArgs A) {
         // Iterations in which every valid lane is still inside its chunk
         // commit without the per-lane select (all of them for equal lengths).
         const uint32_t Tmin = __builtin_amdgcn_readfirstlane(wave_min(valid ? T : 0xffffffffu));
-        const uint32_t full = min(Tmin, units * U) / (2 * U) * (2 * U);
+        const uint32_t full = (V & kVUnmask) ? min(Tmin, units * U) / (2 * U) * (2 * U) : 0u;
         uint32_t k = 0;
         for (; k < full; k += 2 * U) {
-            ConsumeUnits<U, 0, WK, false>::run(k, T, h, Wa, Wb, ring, lane);
+            ConsumeUnits<U, 0, V, false>::run(k, T, h, Wa, Wb, ring, lane);
         }
         for (; k < units * U; k += 2 * U) {
-            ConsumeUnits<U, 0, WK, true>::run(k, T, h, Wa, Wb, ring, lane);
+            ConsumeUnits<U, 0, V, true>::run(k, T, h, Wa, Wb, ring, lane);
         }
         if (valid) emit(A, en.id, h);
     }
@@ -517,8 +537,15 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     case 1: hipLaunchKernelGGL((sha1_split_kernel<1, 1>), dim3(groups), dim3(128), 0, st, A); break;
     case 2: hipLaunchKernelGGL((sha1_split_kernel<2, 1>), dim3(groups), dim3(128), 0, st, A); break;
     case 3: hipLaunchKernelGGL((sha1_split_kernel<3, 1>), dim3(groups), dim3(128), 0, st, A); break;
-    case 6: hipLaunchKernelGGL((sha1_split_kernel<3, 1, false>), dim3(groups), dim3(128), 0, st, A); break;
-    case 7: hipLaunchKernelGGL((sha1_split_kernel<2, 1, false>), dim3(groups), dim3(128), 0, st, A); break;
+#define SPLIT_V(U, V)                                                                             \
+    case 10 * U + V:                                                                              \
+        hipLaunchKernelGGL((sha1_split_kernel<U, 1, V>), dim3(groups), dim3(128), 0, st, A);   \
+        break;
+    // A/B variants: unit 10*U + V (V = kVWK | kVRtSlot | kVUnmask bits)
+    SPLIT_V(3, 0) SPLIT_V(3, 1) SPLIT_V(3, 2) SPLIT_V(3, 3) SPLIT_V(3, 4) SPLIT_V(3, 6)
+    SPLIT_V(3, 7) SPLIT_V(2, 0) SPLIT_V(2, 1) SPLIT_V(2, 2) SPLIT_V(2, 3) SPLIT_V(2, 4) SPLIT_V(2, 6)
+    SPLIT_V(2, 7)
+#undef SPLIT_V
     case 4:  // 4 pairs per workgroup (512 threads), one consumer + producer per SIMD
         hipLaunchKernelGGL((sha1_split_kernel<1, 4>), dim3((groups + 3) / 4), dim3(512), 0, st, A);
         break;

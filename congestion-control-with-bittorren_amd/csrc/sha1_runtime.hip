@@ -199,7 +199,7 @@ int choose_kernel(int kernel, size_t n, int cus) {
 int split_unit(size_t n, int cus) {
     if (const char* e = getenv("SHA1CHUNK_SPLIT_UNIT")) {
         const int u = atoi(e);
-        if (u >= 1 && u <= 7) return u;
+        if ((u >= 1 && u <= 5) || (u >= 20 && u <= 37)) return u;
     }
     const size_t groups = (n + 63) / 64;
     if (groups <= size_t(cus)) return 3;

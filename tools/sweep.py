@@ -29,7 +29,10 @@ def main():
     import torch
     pkg = importlib.import_module("congestion-control-with-bittorren_amd")
     if a.lib:
+        import ctypes
         pkg.sha1chunk.LIB_PATH = os.path.abspath(a.lib)
+        old = ctypes.CDLL(pkg.sha1chunk.LIB_PATH)  # an older build: bind what it has
+        pkg.sha1chunk._SIGNATURES[:] = [sg for sg in pkg.sha1chunk._SIGNATURES if hasattr(old, sg[0])]
     torch.cuda.set_device(0)
     pkg.set_device(0)
     L = a.chunk_len
