@@ -31,6 +31,7 @@ L512 = 524288
 
 def timed(fn, reps=3):
     import torch
+    fn()  # warm-up (first launch of a kernel / first touch of the buffers)
     ts = []
     for _ in range(reps):
         torch.cuda.synchronize()
