@@ -257,6 +257,39 @@ bool host_pinned(const void* p) {
     return at.type == hipMemoryTypeHost;
 }
 
+// Pack a slot's chunks from pageable caller memory into pinned staging with
+// several threads: one thread copies ~10 GB/s, well under the PCIe rate.
+void pack_parallel(uint8_t* h, const uint64_t* hoff, const uint8_t* base, const uint64_t* offsets,
+                   const uint32_t* lengths, const std::vector<uint32_t>& ids, size_t bytes) {
+    static const int kThreads = [] {
+        const char* e = getenv("SHA1CHUNK_COPY_THREADS");
+        return e ? std::max(1, atoi(e)) : 8;
+    }();
+    const size_t m = ids.size();
+    const int T = static_cast<int>(std::min<size_t>(kThreads, std::max<size_t>(1, bytes >> 24)));
+    auto work = [&](size_t j0, size_t j1) {
+        for (size_t j = j0; j < j1; ++j)
+            if (lengths[ids[j]]) memcpy(h + hoff[j], base + offsets[ids[j]], lengths[ids[j]]);
+    };
+    if (T == 1) {
+        work(0, m);
+        return;
+    }
+    // contiguous entry ranges of about bytes/T each
+    std::vector<std::thread> th;
+    size_t j0 = 0;
+    const uint64_t start = hoff[0];
+    for (int t = 1; t < T && j0 < m; ++t) {
+        const uint64_t target = start + bytes * t / T;
+        size_t j1 = j0;
+        while (j1 < m && hoff[j1] < target) ++j1;
+        if (j1 > j0) th.emplace_back(work, j0, j1);
+        j0 = j1;
+    }
+    work(j0, m);
+    for (auto& x : th) x.join();
+}
+
 int stage_and_launch(Device& D, Slot& s, const uint8_t* base, const uint64_t* offsets,
                      const uint32_t* lengths, const std::vector<uint32_t>& order, size_t lo,
                      size_t hi, size_t data_bytes, bool src_pinned) {
@@ -289,10 +322,10 @@ int stage_and_launch(Device& D, Slot& s, const uint8_t* base, const uint64_t* of
             hoff[j] = meta + (offsets[id] - span0);
         } else {
             hoff[j] = cur;
-            if (L) memcpy(h + cur, base + offsets[id], L);
             cur += round_up(L, kAlign);
         }
     }
+    if (!direct) pack_parallel(h, hoff, base, offsets, lengths, s.ids, cur - meta);
     uint8_t* d = static_cast<uint8_t*>(s.dmem.p);
     if (direct) {
         HIP_TRY(hipMemcpyAsync(d, h, meta, hipMemcpyHostToDevice, D.copy));

@@ -142,6 +142,15 @@ def main():
         sec, ts = timed(run, reps=2)
         ok = hashlib.sha1(out["d"].tobytes()).hexdigest() == golden["config3"]["agg"]
         res["config3_pinned_e2e"] = row(n, sec, ts, ok, mode="pinned host -> H2D || hash || D2H")
+        # the same pipeline from PAGEABLE memory (numpy copy of the first
+        # 8192 chunks): slots are packed into pinned staging by host threads
+        m = 8192
+        pageable = np.array(hv[: m * L512])
+        out2 = {}
+        sec_p, ts_p = timed(lambda: out2.update(d=pkg.hash_batch(pageable, off[:m], ln[:m])), reps=2)
+        ok_p = bool(np.array_equal(out2["d"], out["d"][:m]))
+        res["config3_pageable_e2e"] = row(m, sec_p, ts_p, ok_p, mode="pageable host -> pack || H2D || hash || D2H")
+        del pageable
         # raw PCIe rate on this box for the same bytes, for context
         dev = torch.empty(1 << 30, dtype=torch.uint8, device="cuda")
         sec_c, _ = timed(lambda: dev.copy_(host[: 1 << 30], non_blocking=True), reps=3)
