@@ -44,6 +44,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 # (measured, tools/microbench.hip -> profiles/microbench_issue_r01.json) at
 # the 2.4 GHz the chip holds at this occupancy.
 ROUND_VALU_PER_BLOCK = 400
+# The split consumer's whole per-block stream (400 round ops + 20 ds_read_b128
+# of the schedule + 5 feed-forward adds + loop/barrier scalars), counted in
+# the unrolled 6-block loop of sha1_split_kernel<3,1> (`make isa`).
+CONSUMER_INSTR_PER_BLOCK = 429
 ISSUE_CYCLES = 4.63
 CLOCK_HZ = 2.4e9
 
@@ -147,6 +151,7 @@ def main():
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     blocks = (L + 8) // 64 + 1  # SHA-1 compressions per chunk (sha.c:536-543 padding)
     floor_ms = blocks * ROUND_VALU_PER_BLOCK * ISSUE_CYCLES / CLOCK_HZ * 1e3
+    stream_ms = blocks * CONSUMER_INSTR_PER_BLOCK * ISSUE_CYCLES / CLOCK_HZ * 1e3
 
     result = {
         "metric": METRIC,
@@ -179,6 +184,9 @@ def main():
             "floor_ms": round(floor_ms, 4), "achieved_ms": round(kern_ms, 4),
             "frac": round(floor_ms / kern_ms, 4),
             "model": f"{blocks} blocks x {ROUND_VALU_PER_BLOCK} VALU x {ISSUE_CYCLES} cyc / 2.4 GHz",
+            "stream_floor_ms": round(stream_ms, 4), "stream_frac": round(stream_ms / kern_ms, 4),
+            "stream_model": f"{blocks} blocks x {CONSUMER_INSTR_PER_BLOCK} consumer instructions "
+                            f"x {ISSUE_CYCLES} cyc / 2.4 GHz",
         },
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
