@@ -15,7 +15,8 @@ struct BatchArgs {
     uint32_t n;
     const uint32_t* order;
     uint8_t* dig;  // n x 20 digest bytes (finalising mode), 4-byte aligned
-    // Streaming extras (lane kernel only; null/0 for plain batches):
+    // Streaming extras (null/0 for plain batches).  init_state/out_state:
+    // every kernel; prefix_bytes (finalising a stream): lane kernel only.
     const uint32_t* init_state;  // 5 words per message instead of the IV
     uint64_t prefix_bytes;       // bytes already hashed before this call
     uint32_t* out_state;         // non-null: no padding, write raw state

@@ -365,7 +365,8 @@ __global__ __launch_bounds__(128 * PAIRS) void sha1_split_kernel(BatchArgs A) {
     const bool valid = e < A.n;
     Entry en = fetch_entry(A, valid ? e : min(group * 64u, A.n - 1u));
     if (!valid) en.len = 0;
-    const uint32_t T = valid ? total_blocks(en.len) : 0u;
+    // update mode (A.out_state): whole blocks only, no padding
+    const uint32_t T = valid ? (A.out_state ? (en.len >> 6) : total_blocks(en.len)) : 0u;
     uint32_t Tmax = __builtin_amdgcn_readfirstlane(wave_max(T));
     if constexpr (PAIRS > 1) {
         // workgroup max through the (not yet used) ring; the second barrier
@@ -410,7 +411,7 @@ __global__ __launch_bounds__(128 * PAIRS) void sha1_split_kernel(BatchArgs A) {
     } else {
         // ----------------------------- consumer -------------------------
         uint32_t h[5];
-        init_state(h);
+        load_init(A, en.id, h);
         uint32_t Wa[80], Wb[80];
         split_barrier();  // B_0
         read_w_group<0>(ring + lane * 16, Wa);
@@ -458,7 +459,7 @@ __global__ __launch_bounds__(256) void sha1_fused_kernel(BatchArgs A) {
     Entry en = fetch_entry(A, valid ? e : min(group * 64u, A.n - 1u));
     if (!valid) en.len = 0;
     uint32_t h[5];
-    init_state(h);
+    load_init(A, en.id, h);
     const bool a16 = (reinterpret_cast<uintptr_t>(en.p) & 15u) == 0;
     const uint32_t S = (wave_any(valid) && wave_all(!valid || a16))
                            ? __builtin_amdgcn_readfirstlane(

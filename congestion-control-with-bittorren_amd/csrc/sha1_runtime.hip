@@ -189,6 +189,12 @@ int get_device(Device** out) {
 //    in one wave, 4 blocks of register prefetch) wins.
 int choose_kernel(int kernel, size_t n, int cus) {
     if (kernel != SHA1CHUNK_KERNEL_AUTO) return kernel;
+    // A/B and test hook: force one kernel behind every AUTO call site
+    if (const char* f = getenv("SHA1CHUNK_FORCE_KERNEL")) {
+        if (!strcmp(f, "lane")) return SHA1CHUNK_KERNEL_LANE;
+        if (!strcmp(f, "fused")) return SHA1CHUNK_KERNEL_FUSED;
+        if (!strcmp(f, "split")) return SHA1CHUNK_KERNEL_SPLIT;
+    }
     const size_t groups = (n + 63) / 64;
     return groups <= size_t(cus) * 2 ? SHA1CHUNK_KERNEL_SPLIT : SHA1CHUNK_KERNEL_FUSED;
 }
@@ -501,6 +507,9 @@ int sha1chunk_hash_uniform_async(const void* d_base, uint32_t chunk_len, size_t 
 
 int sha1chunk_compare_device_async(const uint8_t* d_digests, const uint8_t* d_expected, size_t n,
                                    uint8_t* d_mismatch, void* stream) {
+    if (n > 0xffffffffu) return fail(SHA1CHUNK_EINVAL, "n too large");
+    if (n && (!d_digests || !d_expected || !d_mismatch))
+        return fail(SHA1CHUNK_EINVAL, "null device pointer");
     Device* D;
     int rc = get_device(&D);
     if (rc) return rc;
@@ -743,7 +752,7 @@ int sha1chunk_compress_blocks(uint32_t state[5], const void* blocks, size_t nblo
     A.n = 1;
     A.init_state = reinterpret_cast<const uint32_t*>(d);
     A.out_state = reinterpret_cast<uint32_t*>(d + 32);
-    if ((rc = launch_checked(SHA1CHUNK_KERNEL_LANE, A, st))) return rc;
+    if ((rc = launch_checked(choose_kernel(SHA1CHUNK_KERNEL_AUTO, 1, D->cus), A, st, D->cus))) return rc;
     HIP_TRY(hipMemcpyAsync(h + 32, d + 32, 20, hipMemcpyDeviceToHost, st));
     HIP_TRY(hipStreamSynchronize(st));
     memcpy(state, h + 32, 20);

@@ -50,7 +50,13 @@ def test_kats_streaming_trio(pkg, dev, golden):
     assert s.final().hex() == golden["kats"]["million_a"]["digest"]
 
 
-def test_streaming_odd_splits(pkg, dev, oracle):
+@pytest.mark.parametrize("kernel", ["auto", "lane", "fused", "split"])
+def test_streaming_odd_splits(pkg, dev, oracle, kernel, monkeypatch):
+    """SHA1Update/SHA1Final (sha.c:453-558) with the device compressing the
+    whole blocks of each update on every kernel (update mode: IV or chained
+    state in, raw state out, no padding)."""
+    if kernel != "auto":
+        monkeypatch.setenv("SHA1CHUNK_FORCE_KERNEL", kernel)
     rng = np.random.default_rng(9)
     data = rng.integers(0, 256, 20000, dtype=np.uint8).tobytes()
     for cuts in ([1, 63, 64, 65, 1000, 130], [7] * 40, [0, 19999]):
@@ -61,6 +67,12 @@ def test_streaming_odd_splits(pkg, dev, oracle):
             pos += c
         s.update(data[pos:])
         assert s.final() == oracle.shahash(data)
+    # one large update (bulk stages) after an unaligned prefix
+    big = rng.integers(0, 256, 3 * 524288 + 77, dtype=np.uint8).tobytes()
+    s = pkg.SHA1()
+    s.update(big[:5])
+    s.update(big[5:])
+    assert s.final() == oracle.shahash(big)
 
 
 def test_edge_lengths_all_kernels(pkg, dev, oracle, golden):
