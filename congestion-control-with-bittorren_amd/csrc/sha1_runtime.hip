@@ -225,6 +225,8 @@ hipError_t launch(int kernel, const BatchArgs& A, int cus, hipStream_t st) {
 int launch_checked(int kernel, const BatchArgs& A, hipStream_t st, int cus = 256) {
     if (kernel < SHA1CHUNK_KERNEL_LANE || kernel > SHA1CHUNK_KERNEL_SPLIT)
         return fail(SHA1CHUNK_EINVAL, "unknown kernel id %d", kernel);
+    if (A.n > 0xffffffffu - 1024u)  // grid sizes are computed in 32 bits
+        return fail(SHA1CHUNK_EINVAL, "batch of %u chunks: at most 2^32 - 1025 per call", A.n);
     if (A.n > 0 && (reinterpret_cast<uintptr_t>(A.dig) & 3u))
         return fail(SHA1CHUNK_EALIGN, "digest buffer must be 4-byte aligned");
     hipError_t e = launch(kernel, A, cus, st);
