@@ -46,8 +46,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 ROUND_VALU_PER_BLOCK = 400
 # The split consumer's whole per-block stream (400 round ops + 20 ds_read_b128
 # of the schedule + 5 feed-forward adds + loop/barrier scalars), counted in
-# the unrolled 6-block loop of sha1_split_kernel<3,1> (`make isa`).
-CONSUMER_INSTR_PER_BLOCK = 429
+# the unrolled 8-block loop of sha1_split_kernel<4,1> (`make isa`).
+CONSUMER_INSTR_PER_BLOCK = 428
 ISSUE_CYCLES = 4.63
 CLOCK_HZ = 2.4e9
 

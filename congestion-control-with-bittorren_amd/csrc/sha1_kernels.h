@@ -24,7 +24,8 @@ struct BatchArgs {
 
 hipError_t launch_lane(const BatchArgs& A, hipStream_t st);
 hipError_t launch_fused(const BatchArgs& A, hipStream_t st);
-// unit_blocks (1..3): schedule blocks per producer/consumer barrier; LDS = unit_blocks * 40 KiB
+// unit_blocks 1..4: schedule blocks per producer/consumer barrier (LDS = unit_blocks * 40 KiB);
+// 8, 9: multi-pair workgroups; 10*U+V: variant flags (sha1_kernels.hip)
 hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st);
 hipError_t launch_synth(uint8_t* dst, const uint64_t* off, const uint32_t* lens, uint32_t ulen,
                         uint64_t first, uint64_t count, uint64_t seed, hipStream_t st);

@@ -154,8 +154,9 @@ __global__ __launch_bounds__(256) void sha1_lane_kernel(BatchArgs A) {
 //   RAW: unit m+1 is complete before B_{m+1}; its reads come after it.
 //   WAR: the producer rewrites slot m&1 (unit m+2) only after B_{m+1}; every
 //        read of unit m was issued before B_{m+1} and drained by its lgkmcnt(0).
-// Fewer barriers per block (U > 1) is worth ~10% at low occupancy; U = 1
-// keeps LDS at 40 KiB for higher occupancy.
+// Fewer barriers per block (U > 1) is worth ~10% at low occupancy (U = 4,
+// the whole 160 KiB LDS, is ~1.5% ahead of U = 3); U = 1 keeps LDS at 40 KiB
+// for higher occupancy.
 constexpr int kWBlockBytes = 20 * 1024;
 
 // The lgkmcnt(0) goes through the builtin so hipcc knows every LDS access
@@ -283,7 +284,7 @@ constexpr int kVUnmask = 4;  // unmasked commit while every lane is live
 // faster; with 2-block units W+K wins (by ~5%) and the slot form does not
 // matter.  Unmasked commit helps both.
 template <int U>
-constexpr int kSplitV = U == 3 ? (kVRtSlot | kVUnmask) : (kVWK | kVUnmask);
+constexpr int kSplitV = U >= 3 ? (kVRtSlot | kVUnmask) : (kVWK | kVUnmask);
 
 template <int U, int J, int V, bool MASK>
 __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (&h)[5],
@@ -538,6 +539,7 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     case 1: hipLaunchKernelGGL((sha1_split_kernel<1, 1>), dim3(groups), dim3(128), 0, st, A); break;
     case 2: hipLaunchKernelGGL((sha1_split_kernel<2, 1>), dim3(groups), dim3(128), 0, st, A); break;
     case 3: hipLaunchKernelGGL((sha1_split_kernel<3, 1>), dim3(groups), dim3(128), 0, st, A); break;
+    case 4: hipLaunchKernelGGL((sha1_split_kernel<4, 1>), dim3(groups), dim3(128), 0, st, A); break;
 #define SPLIT_V(U, V)                                                                             \
     case 10 * U + V:                                                                              \
         hipLaunchKernelGGL((sha1_split_kernel<U, 1, V>), dim3(groups), dim3(128), 0, st, A);   \
@@ -545,12 +547,12 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     // A/B variants: unit 10*U + V (V = kVWK | kVRtSlot | kVUnmask bits)
     SPLIT_V(3, 0) SPLIT_V(3, 1) SPLIT_V(3, 2) SPLIT_V(3, 3) SPLIT_V(3, 4) SPLIT_V(3, 6)
     SPLIT_V(3, 7) SPLIT_V(2, 0) SPLIT_V(2, 1) SPLIT_V(2, 2) SPLIT_V(2, 3) SPLIT_V(2, 4) SPLIT_V(2, 6)
-    SPLIT_V(2, 7)
+    SPLIT_V(2, 7) SPLIT_V(4, 2) SPLIT_V(4, 4) SPLIT_V(4, 5)
 #undef SPLIT_V
-    case 4:  // 4 pairs per workgroup (512 threads), one consumer + producer per SIMD
+    case 8:  // 4 pairs per workgroup (512 threads), one consumer + producer per SIMD
         hipLaunchKernelGGL((sha1_split_kernel<1, 4>), dim3((groups + 3) / 4), dim3(512), 0, st, A);
         break;
-    case 5:  // 2 pairs per workgroup, 2-block units
+    case 9:  // 2 pairs per workgroup, 2-block units
         hipLaunchKernelGGL((sha1_split_kernel<2, 2>), dim3((groups + 1) / 2), dim3(256), 0, st, A);
         break;
     default: return hipErrorInvalidValue;

@@ -199,16 +199,17 @@ int choose_kernel(int kernel, size_t n, int cus) {
     return groups <= size_t(cus) * 2 ? SHA1CHUNK_KERNEL_SPLIT : SHA1CHUNK_KERNEL_FUSED;
 }
 
-// Split-kernel shape: 3-block units (1 barrier per 3 blocks, 120 KiB LDS) at
-// one workgroup per CU, 2-block units (80 KiB) at two per CU, else 1-block
-// units (40 KiB).  SHA1CHUNK_SPLIT_UNIT overrides (1..5, see launch_split).
+// Split-kernel shape: 4-block units (1 barrier per 4 blocks, the whole 160
+// KiB LDS) at one workgroup per CU, 2-block units (80 KiB) at two per CU,
+// else 1-block units (40 KiB).  SHA1CHUNK_SPLIT_UNIT overrides (1..4 units,
+// 8/9 multi-pair shapes, 10*U+V variants; see launch_split).
 int split_unit(size_t n, int cus) {
     if (const char* e = getenv("SHA1CHUNK_SPLIT_UNIT")) {
         const int u = atoi(e);
-        if ((u >= 1 && u <= 5) || (u >= 20 && u <= 37)) return u;
+        if ((u >= 1 && u <= 4) || u == 8 || u == 9 || (u >= 20 && u <= 47)) return u;
     }
     const size_t groups = (n + 63) / 64;
-    if (groups <= size_t(cus)) return 3;
+    if (groups <= size_t(cus)) return 4;
     if (groups <= size_t(cus) * 2) return 2;
     return 1;
 }
