@@ -36,14 +36,14 @@ def read_chunk(path: str | os.PathLike) -> list[str]:
     """chunk.c:93-115.  For every line whose first space-separated token
     starts with a digit, the second token with one trailing '\\n' removed
     (a CRLF file keeps its '\\r', as in the reference; the peer compares the
-    first 40 characters only).  Other lines print the reference's notice."""
+    first 40 characters only).  Other lines, and a digit line without a
+    second token (the reference dereferences NULL there), print the
+    reference's notice.  Same rules as read_chunk in csrc/chunk_file.c."""
     out = []
     with open(path, "r", newline="") as f:
         for line in f:
             toks = [t for t in line.split(" ") if t != ""]
-            if toks and toks[0][:1].isdigit():
-                if len(toks) < 2:
-                    raise ValueError(f"{path}: chunk line without a hash: {line!r}")
+            if len(toks) >= 2 and toks[0][:1].isdigit():
                 tok = toks[1]
                 out.append(tok[:-1] if tok.endswith("\n") else tok)
             else:

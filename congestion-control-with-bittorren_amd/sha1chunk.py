@@ -74,6 +74,12 @@ _SIGNATURES = [
     ("get_chunk_hash", C.c_void_p, [C.c_char_p, C.c_size_t]),
     ("verify_chunk_hash", None, [_vp, C.c_char_p, C.c_size_t]),
     ("verify_hash", C.c_int, [C.c_char_p, C.c_char_p]),
+    # non-hash rest of chunk.h (csrc/chunk_file.c); read_chunk appends to the
+    # peer's vector through the peer's vec_add, so it is called from C only
+    ("read_chunk", None, [C.c_char_p, _vp]),
+    ("find_chunk_idx_from_hash", C.c_size_t, [C.c_char_p, C.c_char_p]),
+    ("seek_to_chunk_pos", None, [_vp, C.c_size_t]),
+    ("seek_to_packet_pos", None, [_vp, C.c_size_t, C.c_size_t]),
     ("sha1chunk_hash_batch", C.c_int, [_vp, _u64p, _u32p, C.c_size_t, _u8p, C.c_uint]),
     ("sha1chunk_verify_batch", C.c_int, [_vp, _u64p, _u32p, C.c_size_t, _u8p, _u8p, C.c_uint]),
     ("sha1chunk_hash_device_async", C.c_int, [_vp, _vp, _vp, C.c_size_t, _vp, _vp, C.c_int]),

@@ -11,8 +11,12 @@
  *   verify_chunk_hash  chunk.h:50  (chunk.c:204-217) sender-side check, exit(-1) on mismatch
  *   get_chunk_hash     chunk.h:51  (chunk.c:168-185) malloc'd hex digest, caller frees
  *   verify_hash        job.h:65    (job.c:217-228)   0 = match, 1 = mismatch
- * The non-hash helpers of chunk.h (read_chunk, find_chunk_idx_from_hash,
- * seek_to_*) stay in the peer's chunk.c; see INTEGRATION.md.
+ * and the non-hash rest of chunk.h, so the peer links without chunk.o
+ * (csrc/chunk_file.c):
+ *   read_chunk                chunk.h:46  (chunk.c:93-115)   hash column -> peer's vector
+ *   find_chunk_idx_from_hash  chunk.h:47  (chunk.c:123-160)  (size_t)-1 when absent
+ *   seek_to_chunk_pos         chunk.h:48  (chunk.c:192-196)
+ *   seek_to_packet_pos        chunk.h:49  (chunk.c:226-233)
  */
 #ifndef SHA1CHUNK_CHUNK_HASH_H
 #define SHA1CHUNK_CHUNK_HASH_H
@@ -41,6 +45,14 @@ void hex2binary(char *hex, int len, uint8_t *buf);
 void verify_chunk_hash(FILE *f, char *requested_chunk_hash, size_t chunk_idx);
 char *get_chunk_hash(char *chunk, size_t size);
 int verify_hash(char *chunk_hash, char *data);
+
+/* The peer's vector (utility.h:16-21); read_chunk appends through the
+ * peer's own vec_add (utility.c:22-34), resolved from the executable. */
+struct vector;
+void read_chunk(char *filename, struct vector *v);
+size_t find_chunk_idx_from_hash(char *chunk_hash, char *hash_chunk_file);
+void seek_to_chunk_pos(FILE *f, size_t chunk_idx);
+void seek_to_packet_pos(FILE *f, size_t chunk_idx, size_t last_sent_packet);
 
 #ifdef __cplusplus
 }

@@ -120,6 +120,24 @@ def test_make_chunks_cli_reproduces_C_chunks(pkg, dev, golden, fixture_files, tm
     assert out == want  # tmp/C.chunks with CRLF stripped
 
 
+def test_reference_make_chunks_main_dropin(pkg, dev, golden, fixture_files, tmp_path):
+    """The reference's own make_chunks.c main, unmodified, linked without
+    chunk.o/sha.o against libsha1chunk.so (oracle/Makefile `dropin`, built in
+    the container from /root/reference): its output on the reference's
+    fixture files equals the reference's make-chunks output."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "dropin", "make-chunks")
+    if not os.path.exists(exe):
+        pytest.skip("drop-in make-chunks was not built (needs /root/reference at build time)")
+    fixtures = {"tmp/C.tar": golden["fixtures"]["C.chunks_file"]}
+    fixtures.update(golden["fixtures"]["make_chunks"])
+    for name, want in fixtures.items():
+        p = tmp_path / os.path.basename(name)
+        p.write_bytes(fixture_files[name])
+        r = subprocess.run([exe, str(p)], capture_output=True, text=True, timeout=60)
+        assert r.returncode == 0, r.stderr
+        assert r.stdout == "".join(f"{i} {h}\n" for i, h in enumerate(want)), name
+
+
 def test_verify_hash_semantics(pkg, dev, golden, fixture_files, capfd):
     data = fixture_files["tmp/C.tar"][:L512]
     good = golden["fixtures"]["C.chunks_file"][0]
