@@ -50,6 +50,12 @@ ROUND_VALU_PER_BLOCK = 400
 CONSUMER_INSTR_PER_BLOCK = 428
 ISSUE_CYCLES = 4.63
 CLOCK_HZ = 2.4e9
+# VALU-int roofline: the algorithmic SHA-1 op count per 64-B
+# block (80 x 5 round ops + 64 x 3 schedule ops + 16 byte swaps + 5
+# feed-forward adds) against the chip's int32 lane-op rate, 256 CU x 4 SIMD
+# x 16 lanes x 2.4 GHz.
+VALU_OPS_PER_BLOCK = 613
+VALU_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
 
 
 def parse():
@@ -151,6 +157,7 @@ def main():
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     blocks = (L + 8) // 64 + 1  # SHA-1 compressions per chunk (sha.c:536-543 padding)
     floor_ms = blocks * ROUND_VALU_PER_BLOCK * ISSUE_CYCLES / CLOCK_HZ * 1e3
+    valu_tops = n * blocks * VALU_OPS_PER_BLOCK / (kern_ms * 1e-3) / 1e12  # one chunk per lane
     stream_ms = blocks * CONSUMER_INSTR_PER_BLOCK * ISSUE_CYCLES / CLOCK_HZ * 1e3
 
     result = {
@@ -178,6 +185,11 @@ def main():
             "frac": round(achieved / HBM_PEAK_GBS, 5),
             "traffic": _traffic(n, L),
             "kernel_ms": round(kern_ms, 4),
+        },
+        "valu_roofline": {
+            "achieved": round(valu_tops, 3), "peak": round(VALU_PEAK_TOPS, 2),
+            "unit": "T int32 lane-ops/s", "frac": round(valu_tops / VALU_PEAK_TOPS, 4),
+            "ops_per_block": VALU_OPS_PER_BLOCK,
         },
         "serial_bound": {
             "bound": "per-chunk serial VALU issue (rounds-only wave)",
