@@ -10,7 +10,7 @@
 //
 // How it maps to CDNA4 (one SHA-1 message per lane; 64 messages per wave):
 //   rotate            -> v_alignbit_b32 (1 op)
-//   Ch/Parity/Maj     -> v_bitop3_b32 (one op each)
+//   Ch                -> v_bfi_b32 (compiler pattern)  Parity/Maj -> v_bitop3_b32
 //   5-term round sum  -> 2 x v_add3_u32
 //   schedule xor4     -> v_bitop3_b32(xor3) + v_xor_b32, then v_alignbit_b32
 //   byte swap         -> v_perm_b32
@@ -35,11 +35,14 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 __device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
 }
-// Ch = b ? c : d.  v_bitop3 (table 0xCA) rather than the v_bfi_b32 hipcc
-// selects for d ^ (b & (c ^ d)): both are one VALU, but bitop3 is in the
-// ~1.1 ns SIMD-time class and bfi in the ~1.9 ns class (microbench_ops_r01).
+// Ch = b ? c : d -> v_bfi_b32 (compiler pattern).  v_bitop3 (table 0xCA) is
+// also one VALU and in the faster SIMD-time class, but measured A/B on
+// MI355X it made the split consumer 3% slower (7.06 vs 6.85 ms at 4096
+// chunks: hipcc schedules the Ch right before its add3 and bitop3's result
+// latency is not hidden by one wave) and left the fused kernel unchanged
+// (profiles/ch_bitop3_ab_r01.json).
 __device__ __forceinline__ uint32_t chf(uint32_t b, uint32_t c, uint32_t d) {
-    return __builtin_amdgcn_bitop3_b32(b, c, d, 0xCA);
+    return d ^ (b & (c ^ d));
 }
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
 

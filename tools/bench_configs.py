@@ -88,6 +88,26 @@ def main():
         sec, ts, d = uniform(262144, reps=2)
         res["config4_one_gpu"] = row(262144, sec, ts,
                                      hashlib.sha1(d.tobytes()).hexdigest() == golden["config4"]["agg"])
+        # Strong scaling of the fixed 262144-chunk job:
+        # shards are equal and independent (no collective), so N GPUs take
+        # as long as one GPU takes for its 262144/N-chunk shard.  Projected
+        # from one GPU; the driver's multi-GPU runs measure the real thing.
+        strong = {"1": {"shard_s": res["config4_one_gpu"]["seconds"]},
+                  "8": {"shard_s": res["config4_shard"]["seconds"]}}
+        for N in (2, 4):
+            n = 262144 // N
+            sec, ts, d = uniform(n, first=n, reps=2)
+            res[f"config4_shard_of_{N}"] = row(
+                n, sec, ts, hashlib.sha1(d.tobytes()).hexdigest() == golden["config4"]["shard_aggs"][str(N)][1],
+                note=f"rank 1 of {N}")
+            strong[str(N)] = {"shard_s": res[f"config4_shard_of_{N}"]["seconds"]}
+        t1 = strong["1"]["shard_s"]
+        for N, r in sorted(strong.items(), key=lambda kv: int(kv[0])):
+            r["projected_GiBps"] = round(262144 * L512 / r["shard_s"] / 2**30, 1)
+            r["speedup"] = round(t1 / r["shard_s"], 3)
+            r["efficiency"] = round(t1 / r["shard_s"] / int(N), 3)
+        res["config4_strong_projection"] = dict(sorted(strong.items(), key=lambda kv: int(kv[0])))
+        print(json.dumps({"config4_strong_projection": res["config4_strong_projection"]}), flush=True)
 
     if "occupancy" not in skip:
         for n in (65536, 131072):
