@@ -104,7 +104,7 @@ struct Slot {
 
 struct Device {
     std::mutex mu;
-    bool ready = false;
+    std::atomic<bool> ready{false};  // set once, under mu, after the streams exist
     int id = -1;
     int cus = 256;
     Slot slot[2];
@@ -160,9 +160,9 @@ int get_device(Device** out) {
     if (t_dev < 0 || t_dev >= g_count) return fail(SHA1CHUNK_EINVAL, "bad device %d", t_dev);
     Device& D = g_dev[t_dev];
     HIP_TRY(hipSetDevice(D.id));
-    if (!D.ready) {
+    if (!D.ready.load(std::memory_order_acquire)) {
         std::lock_guard<std::mutex> lk(D.mu);
-        if (!D.ready) {
+        if (!D.ready.load(std::memory_order_relaxed)) {
             hipDeviceProp_t pr;
             HIP_TRY(hipGetDeviceProperties(&pr, D.id));
             D.cus = pr.multiProcessorCount;
@@ -172,7 +172,7 @@ int get_device(Device** out) {
                 HIP_TRY(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
             }
             HIP_TRY(hipStreamCreateWithFlags(&D.copy, hipStreamNonBlocking));
-            D.ready = true;
+            D.ready.store(true, std::memory_order_release);
         }
     }
     *out = &D;
@@ -358,6 +358,18 @@ int stage_and_launch(Device& D, Slot& s, const uint8_t* base, const uint64_t* of
     return SHA1CHUNK_OK;
 }
 
+// A call that failed half-way can leave a slot in flight; its results
+// belong to that call, so the next call waits for the work and drops them
+// instead of scattering stale digests into its own output.
+int discard_in_flight(Device& D) {
+    for (auto& s : D.slot) {
+        if (!s.busy) continue;
+        s.busy = false;
+        HIP_TRY(hipEventSynchronize(s.done));
+    }
+    return SHA1CHUNK_OK;
+}
+
 int drain(Slot& s, uint8_t* digests) {
     if (!s.busy) return SHA1CHUNK_OK;
     s.busy = false;
@@ -373,6 +385,7 @@ int hash_host(const uint8_t* base, const uint64_t* offsets, const uint32_t* leng
     int rc = get_device(&D);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(D->mu);
+    if ((rc = discard_in_flight(*D))) return rc;
     // Longest first, so every wave of 64 gets near-equal lengths (a wave
     // runs as long as its longest lane); equal lengths keep caller order.
     std::vector<uint32_t> order(n);
@@ -579,6 +592,7 @@ long sha1chunk_hash_stream(sha1chunk_reader_fn reader, void* reader_ctx, sha1chu
     int rc = get_device(&D);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(D->mu);
+    if ((rc = discard_in_flight(*D))) return rc;
     const size_t per_slot = kSlotBytes / SHA1CHUNK_CHUNK_LEN;  // 512 chunks per slot
     const size_t meta = round_up(per_slot * 12, kAlign);
     size_t next = 0;  // index of the next slot's first chunk
