@@ -318,6 +318,29 @@ def test_config3_device_resident_aggregate(pkg, dev, oracle, golden):
     del buf
 
 
+def test_config4_whole_on_one_gpu(pkg, dev, oracle, golden):
+    """The largest BASELINE corpus, all 262144 x 512 KiB chunks (128 GiB)
+    resident on one GPU, hashed in one launch (fused kernel regime): the
+    digest-of-digests and every per-rank shard aggregate of the 1/2/4/8-way
+    splits equal the reference's."""
+    torch = dev
+    n = 262144
+    buf = torch.empty(n * L512, dtype=torch.uint8, device="cuda")
+    pkg.synth_fill_device(buf, 0, n, L512)
+    dig = torch.zeros((n, 20), dtype=torch.uint8, device="cuda")
+    pkg.hash_uniform_device(buf, L512, n, dig)
+    torch.cuda.synchronize()
+    del buf
+    torch.cuda.empty_cache()
+    got = dig.cpu().numpy()
+    assert _agg(oracle, got) == golden["config4"]["agg"]
+    for N, aggs in golden["config4"]["shard_aggs"].items():
+        per = n // int(N)
+        assert [_agg(oracle, got[r * per:(r + 1) * per]) for r in range(int(N))] == aggs, N
+    # and bench.py's weak-scaling ranks (4096 chunks each)
+    assert [_agg(oracle, got[r * 4096:(r + 1) * 4096]) for r in range(8)] == golden["weak4096"]
+
+
 def test_host_batch_all_devices(pkg, dev, oracle, golden):
     n = 512
     host = oracle.synth_chunks(0, n)
