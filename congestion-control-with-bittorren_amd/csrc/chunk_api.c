@@ -281,7 +281,8 @@ static int master_lookup(FILE *f, size_t idx, uint8_t out20[20], off_t *size) {
         uint8_t *tab = (uint8_t *)malloc(20 * n);
         if (tab) {
             padded_reader r = {fd, 0, st.st_size, (off_t)n * CHUNK_LEN};
-            long got = sha1chunk_hash_stream(padded_read, &r, index_sink, tab);
+            long got = sha1chunk_hash_stream_sized(padded_read, &r, index_sink, tab,
+                                                   (uint64_t)n * CHUNK_LEN);
             if (got < 0) die("verify_chunk_hash index", (int)got);
             if ((size_t)got == n && r.size == st.st_size) {
                 master.digest = tab;

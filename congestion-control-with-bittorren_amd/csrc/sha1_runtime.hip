@@ -51,7 +51,32 @@ int fail(int code, const char* fmt, ...) {
     } while (0)
 
 constexpr size_t kAlign = 128;  // device layout: every chunk starts on a 128-B line
-constexpr size_t kSlotBytes = size_t(256) << 20;  // host-batch pipeline slot (256 MiB)
+// Stream (file) pipeline: a ring of slots, each read into pinned memory,
+// copied H2D and hashed on its own stream.  A slot's kernel takes ~7 ms
+// however few chunks it holds (one chunk's serial chain), so slots must be
+// large (512 MiB: ~10 ms of PCIe) and several in flight: with 2 slots each
+// read waited for the kernel 2 slots back.  3 slots keep the slot streams
+// plus the copy stream within the process's 4 hardware queues (more streams
+// share queues and serialise kernels).  Measured on an 8 GiB file in the
+// page cache (profiles/file_vq_r01.json): 2 x 256 MiB 29.6 GiB/s, 3 x 512 MiB
+// 47.9 GiB/s (PCIe H2D 53.6).
+// SHA1CHUNK_STREAM_SLOTS (2..8) / SHA1CHUNK_STREAM_SLOT_MIB (16..1024) for A/B.
+constexpr int kMaxSlots = 8;
+int stream_slots() {
+    static const int n = [] {
+        const char* e = getenv("SHA1CHUNK_STREAM_SLOTS");
+        return e ? std::min(kMaxSlots, std::max(2, atoi(e))) : 3;
+    }();
+    return n;
+}
+size_t stream_slot_bytes() {
+    static const size_t b = [] {
+        const char* e = getenv("SHA1CHUNK_STREAM_SLOT_MIB");
+        const size_t mib = e ? std::min<size_t>(1024, std::max<size_t>(16, atoi(e))) : 512;
+        return mib << 20;  // a multiple of SHA1CHUNK_CHUNK_LEN
+    }();
+    return b;
+}
 
 inline size_t round_up(size_t x, size_t a) { return (x + a - 1) / a * a; }
 
@@ -107,7 +132,9 @@ struct Device {
     std::atomic<bool> ready{false};  // set once, under mu, after the streams exist
     int id = -1;
     int cus = 256;
-    Slot slot[2];
+    // Host batches use slots 0-1; the stream (file) pipeline cycles through
+    // stream_slots() of them.
+    Slot slot[kMaxSlots];
     // Every slot's H2D goes through this one stream: copies run back to back
     // at the full PCIe rate instead of two slots splitting it (which would
     // delay the first kernel), and the next slot's copy queues behind the
@@ -585,18 +612,33 @@ int sha1chunk_verify_batch(const void* base, const uint64_t* offsets, const uint
     return SHA1CHUNK_OK;
 }
 
-long sha1chunk_hash_stream(sha1chunk_reader_fn reader, void* reader_ctx, sha1chunk_sink_fn sink,
-                           void* sink_ctx) {
+}  // extern "C"
+
+namespace {
+// size_hint: bytes the reader will deliver, when known (regular files);
+// small inputs then get a slot just big enough (the pinned allocation is a
+// one-process cost the make-chunks CLI pays on every run), mid-size inputs
+// are spread over all slots so reads and copies overlap.
+long hash_stream_sized(sha1chunk_reader_fn reader, void* reader_ctx, sha1chunk_sink_fn sink,
+                       void* sink_ctx, uint64_t size_hint) {
     if (!reader) return fail(SHA1CHUNK_EINVAL, "null reader");
     Device* D;
     int rc = get_device(&D);
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(D->mu);
     if ((rc = discard_in_flight(*D))) return rc;
-    const size_t per_slot = kSlotBytes / SHA1CHUNK_CHUNK_LEN;  // 512 chunks per slot
+    const int nslots = stream_slots();
+    size_t slot_bytes = stream_slot_bytes();
+    if (size_hint) {
+        const size_t L = SHA1CHUNK_CHUNK_LEN;
+        const size_t whole = round_up(size_hint, L);
+        const size_t spread = std::max(size_t(64) << 20, round_up(size_hint / nslots, L));
+        slot_bytes = std::min({slot_bytes, whole, spread});
+    }
+    const size_t per_slot = slot_bytes / SHA1CHUNK_CHUNK_LEN;  // 1024 chunks per 512 MiB
     const size_t meta = round_up(per_slot * 12, kAlign);
     size_t next = 0;  // index of the next slot's first chunk
-    size_t pend_first[2] = {0, 0}, pend_m[2] = {0, 0};
+    size_t pend_first[kMaxSlots] = {}, pend_m[kMaxSlots] = {};
     auto finish = [&](int w) -> int {
         Slot& s = D->slot[w];
         if (!s.busy) return SHA1CHUNK_OK;
@@ -610,15 +652,15 @@ long sha1chunk_hash_stream(sha1chunk_reader_fn reader, void* reader_ctx, sha1chu
     while (!eof) {
         Slot& s = D->slot[which];
         if ((rc = finish(which))) return rc;
-        if ((rc = s.hpin.ensure(meta + kSlotBytes)) || (rc = s.dmem.ensure(meta + kSlotBytes)) ||
+        if ((rc = s.hpin.ensure(meta + slot_bytes)) || (rc = s.dmem.ensure(meta + slot_bytes)) ||
             (rc = s.hdig.ensure(per_slot * 20)) || (rc = s.ddig.ensure(per_slot * 20)))
             return rc;
         uint8_t* h = static_cast<uint8_t*>(s.hpin.p);
         // Read straight into pinned memory: the fread loop of make_chunks
         // (chunk.c:22), a slot of 512 chunks at a time.
         size_t got = 0;
-        while (got < kSlotBytes) {
-            const size_t r = reader(reader_ctx, h + meta + got, kSlotBytes - got);
+        while (got < slot_bytes) {
+            const size_t r = reader(reader_ctx, h + meta + got, slot_bytes - got);
             if (r == (size_t)-1) return fail(SHA1CHUNK_EIO, "stream read error");
             if (r == 0) {
                 eof = true;
@@ -652,11 +694,25 @@ long sha1chunk_hash_stream(sha1chunk_reader_fn reader, void* reader_ctx, sha1chu
         pend_first[which] = next;
         pend_m[which] = m;
         next += m;
-        which ^= 1;
+        which = (which + 1) % nslots;
     }
-    if ((rc = finish(which))) return rc;
-    if ((rc = finish(which ^ 1))) return rc;
+    // remaining slots complete in issue order: the sink sees ascending indices
+    for (int k = 0; k < nslots; ++k)
+        if ((rc = finish((which + k) % nslots))) return rc;
     return static_cast<long>(next);
+}
+}  // namespace
+
+extern "C" {
+
+long sha1chunk_hash_stream(sha1chunk_reader_fn reader, void* reader_ctx, sha1chunk_sink_fn sink,
+                           void* sink_ctx) {
+    return hash_stream_sized(reader, reader_ctx, sink, sink_ctx, 0);
+}
+
+long sha1chunk_hash_stream_sized(sha1chunk_reader_fn reader, void* reader_ctx,
+                                 sha1chunk_sink_fn sink, void* sink_ctx, uint64_t size_hint) {
+    return hash_stream_sized(reader, reader_ctx, sink, sink_ctx, size_hint);
 }
 
 namespace {
@@ -737,7 +793,7 @@ long sha1chunk_hash_fd(int fd, uint8_t* digests, size_t max_chunks, size_t* tota
     if (fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && pos >= 0) {
         const char* e = getenv("SHA1CHUNK_READ_THREADS");
         ParFile f{fd, pos, std::max(pos, st.st_size), e ? std::max(1, atoi(e)) : 8};
-        n = sha1chunk_hash_stream(par_reader, &f, fd_sink, &sk);
+        n = hash_stream_sized(par_reader, &f, fd_sink, &sk, static_cast<uint64_t>(f.end - f.pos));
         (void)lseek(fd, f.pos, SEEK_SET);
     } else {
         n = sha1chunk_hash_stream(fd_reader, &fd, fd_sink, &sk);

@@ -86,6 +86,7 @@ _SIGNATURES = [
     ("sha1chunk_hash_uniform_async", C.c_int, [_vp, C.c_uint32, C.c_size_t, _vp, _vp, C.c_int]),
     ("sha1chunk_compare_device_async", C.c_int, [_vp, _vp, C.c_size_t, _vp, _vp]),
     ("sha1chunk_hash_stream", C.c_long, [READER_FN, _vp, SINK_FN, _vp]),
+    ("sha1chunk_hash_stream_sized", C.c_long, [READER_FN, _vp, SINK_FN, _vp, C.c_uint64]),
     ("sha1chunk_hash_fd", C.c_long, [C.c_int, _u8p, C.c_size_t, C.POINTER(C.c_size_t)]),
     ("sha1chunk_compress_blocks", C.c_int, [_u32p, _vp, C.c_size_t]),
     ("sha1chunk_finish", C.c_int, [_u32p, C.c_uint64, _vp, C.c_uint32, _u8p]),

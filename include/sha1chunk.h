@@ -77,8 +77,8 @@ int sha1chunk_compare_device_async(const uint8_t *d_digests, const uint8_t *d_ex
                                    size_t n, uint8_t *d_mismatch, void *stream);
 
 /* Hash a byte stream in 512 KiB chunks (the last one at its true length,
- * as make_chunks does, chunk.c:22-23) through a pinned double-buffered
- * read -> H2D -> hash -> D2H pipeline.  `reader` fills up to n bytes of dst
+ * as make_chunks does, chunk.c:22-23) through a ring of pinned slots:
+ * read -> H2D -> hash -> D2H, slots overlapping.  `reader` fills up to n bytes of dst
  * (pinned memory) and returns the count, 0 at end of stream, or (size_t)-1
  * on error; `sink` receives each completed run of digests in order.
  * Returns the number of chunks (>= 0) or a negative error. */
@@ -87,6 +87,11 @@ typedef void (*sha1chunk_sink_fn)(void *ctx, size_t first_chunk, const uint8_t *
                                   size_t count);
 long sha1chunk_hash_stream(sha1chunk_reader_fn reader, void *reader_ctx, sha1chunk_sink_fn sink,
                            void *sink_ctx);
+/* Same, when the caller knows how many bytes the reader will deliver
+ * (size_hint > 0): slots are sized to the input (a small file does not
+ * allocate 512 MiB pinned slots; a mid-size one is spread over all slots). */
+long sha1chunk_hash_stream_sized(sha1chunk_reader_fn reader, void *reader_ctx,
+                                 sha1chunk_sink_fn sink, void *sink_ctx, uint64_t size_hint);
 /* File-descriptor convenience: up to max_chunks digests into `digests`;
  * *total_chunks (optional) gets the file's chunk count. */
 long sha1chunk_hash_fd(int fd, uint8_t *digests, size_t max_chunks, size_t *total_chunks);

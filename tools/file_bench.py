@@ -68,6 +68,7 @@ def main():
     ap.add_argument("--gib", type=float, default=8.0)
     ap.add_argument("--tail", type=int, default=123457, help="extra bytes: a short last chunk")
     ap.add_argument("--out", default="")
+    ap.add_argument("--reps", type=int, default=3, help="timed runs (median reported)")
     a = ap.parse_args()
     pkg = importlib.import_module("congestion-control-with-bittorren_amd")
     size = int(a.gib * 2**30) + a.tail
@@ -79,13 +80,29 @@ def main():
         read_gibs = max(read_rate(path), read_rate(path))
         h2d = h2d_rate(size)
         pkg.make_chunks(path)  # warm-up: device init, pinned slots
-        t0 = time.perf_counter()
-        digs = pkg.make_chunks(path)
-        py_s = time.perf_counter() - t0
+        py_t = []
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            digs = pkg.make_chunks(path)
+            py_t.append(time.perf_counter() - t0)
+        py_s = float(np.median(py_t))
         exe = os.path.join(ROOT, "congestion-control-with-bittorren_amd", "make-chunks")
-        t0 = time.perf_counter()
-        out = subprocess.run([exe, path], capture_output=True, text=True, check=True).stdout
-        cli_s = time.perf_counter() - t0
+        cli_t = []
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            out = subprocess.run([exe, path], capture_output=True, text=True, check=True).stdout
+            cli_t.append(time.perf_counter() - t0)
+        cli_s = float(np.median(cli_t))
+        # the CLI's fixed cost (process start, HIP init, first slot): a 1-chunk file
+        small = path + ".small"
+        with open(path, "rb") as f, open(small, "wb") as g:
+            g.write(f.read(L))
+        small_t = []
+        for _ in range(a.reps):
+            t0 = time.perf_counter()
+            subprocess.run([exe, small], capture_output=True, text=True, check=True)
+            small_t.append(time.perf_counter() - t0)
+        os.unlink(small)
         lines = out.splitlines()
         ok = len(digs) == nchunks and len(lines) == nchunks
         with open(path, "rb") as f:
@@ -96,7 +113,11 @@ def main():
         row = {"file_bytes": size, "chunks": nchunks,
                "make_chunks_py_GiBps": round(size / py_s / 2**30, 3),
                "make_chunks_cli_GiBps": round(size / cli_s / 2**30, 3),
-               "cli_seconds": round(cli_s, 3), "page_cache_read_GiBps": round(read_gibs, 3),
+               "cli_seconds": round(cli_s, 3), "cli_one_chunk_seconds": round(float(np.median(small_t)), 3),
+               "py_runs_s": [round(t, 4) for t in py_t],
+               "stream_slots": os.environ.get("SHA1CHUNK_STREAM_SLOTS", "default"),
+               "stream_slot_mib": os.environ.get("SHA1CHUNK_STREAM_SLOT_MIB", "default"),
+               "page_cache_read_GiBps": round(read_gibs, 3),
                "pinned_h2d_GiBps": round(h2d, 3), "digests_spot_checked_ok": bool(ok)}
         print(json.dumps(row), flush=True)
         if a.out:
