@@ -138,6 +138,41 @@ def test_reference_make_chunks_main_dropin(pkg, dev, golden, fixture_files, tmp_
         assert r.stdout == "".join(f"{i} {h}\n" for i, h in enumerate(want)), name
 
 
+def test_reference_receive_path_dropin(pkg, dev, golden, fixture_files, tmp_path):
+    """The reference's own job.c (job_init's read_chunk + vec_common,
+    populate_chunks_to_download, verify_hash) and utility.c vectors,
+    unmodified, linked without chunk.o/sha.o against libsha1chunk.so
+    (oracle/dropin_driver.c): every reassembled chunk of C.tar verifies (0),
+    every corrupted copy is rejected (1), chunk ids come from the master
+    chunk file, ownership from the has-chunk file.  Fixture files in the
+    reference's CRLF format, master header sharing a line with chunk 0."""
+    exe = os.path.join(ROOT, "oracle", "_ref", "dropin", "verify_driver")
+    if not os.path.exists(exe):
+        pytest.skip("drop-in driver was not built (needs /root/reference at build time)")
+    hashes = golden["fixtures"]["C.chunks_file"]
+    crlf = lambda lines: "".join(l + "\r\n" for l in lines).encode()
+    data = tmp_path / "C.tar"
+    data.write_bytes(fixture_files["tmp/C.tar"])
+    get = tmp_path / "C.chunks"  # tmp/C.chunks
+    get.write_bytes(crlf(f"{i} {h}" for i, h in enumerate(hashes)))
+    master = tmp_path / "C.masterchunks"  # tmp/C.masterchunks layout
+    master.write_bytes(crlf([f"File: {data} Chunks:0 {hashes[0]}"] +
+                            [f"{i} {h}" for i, h in enumerate(hashes) if i]))
+    has = tmp_path / "A.haschunks"  # tmp/A.haschunks: chunks 0, 1 of C
+    has.write_bytes(crlf(f"{i} {h}" for i, h in enumerate(hashes[:2])))
+    r = subprocess.run([exe, str(data), str(get), str(master), str(has)], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.splitlines()
+    assert "COMMON 2" in lines
+    assert [l for l in lines if l.startswith("TODO")] == \
+        [f"TODO {h} {i} {int(i < 2)}" for i, h in enumerate(hashes)]
+    assert [l for l in lines if l.startswith("VERIFY")] == [f"VERIFY {i} 0 1" for i in range(4)]
+    # job.c:219-220 prints the computed and the expected hash for each check
+    for h in hashes:
+        assert f"calculated hash is {h}" in r.stdout
+
+
 def test_verify_hash_semantics(pkg, dev, golden, fixture_files, capfd):
     data = fixture_files["tmp/C.tar"][:L512]
     good = golden["fixtures"]["C.chunks_file"][0]
