@@ -222,11 +222,15 @@ __device__ __forceinline__ void tail_block_words(const Entry& en, uint32_t k, ui
     }
 }
 
-template <int U, bool WK>
+// NPROD producer waves share the stages (2 blocks each) of a unit: with
+// NPROD = 2 and U = 4 each producer owns one stage per unit, so it ends
+// every unit with its own barrier after the unit's odd block; a single
+// producer ends the unit after block U-1.
+template <int U, bool WK, int NPROD = 1>
 __device__ __forceinline__ void produce_block(uint32_t k, uint32_t (&w)[16], uint8_t* ring, int lane) {
     const uint32_t m = k / U, j = k - m * U;
     SchedWrite<0, WK>::run(w, ring + ((m & 1u) * U + j) * kWBlockBytes, lane);
-    if (j == U - 1) split_barrier();
+    if (NPROD == 1 ? j == U - 1 : (k & 1u) == 1u) split_barrier();
 }
 
 // Two blocks (128 contiguous bytes) of one lane's chunk, loaded per lane.
@@ -245,8 +249,9 @@ __device__ __forceinline__ void load_stage(const uint8_t* p, Stage& st) {
 }
 
 // Producer side of one bulk stage: blocks 2s, 2s+1 from `cur`; once the
-// second block's words are taken, `cur` is refilled with stage s+2.
-template <int U, bool WK>
+// second block's words are taken, `cur` is refilled with this producer's
+// stage after next, s + 2 NPROD.
+template <int U, bool WK, int NPROD = 1>
 __device__ __forceinline__ void produce_stage(const Entry& en, uint32_t s, uint32_t S, Stage& cur,
                                               uint8_t* ring, int lane) {
 #pragma unroll
@@ -254,8 +259,8 @@ __device__ __forceinline__ void produce_stage(const Entry& en, uint32_t s, uint3
         uint32_t w[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) w[j] = bswap(cur.w[16 * half + j]);
-        if (half == 1 && s + 2 < S) load_stage(en.p + 128ull * (s + 2), cur);
-        produce_block<U, WK>(2 * s + half, w, ring, lane);
+        if (half == 1 && s + 2 * NPROD < S) load_stage(en.p + 128ull * (s + 2 * NPROD), cur);
+        produce_block<U, WK, NPROD>(2 * s + half, w, ring, lane);
     }
 }
 
@@ -278,13 +283,25 @@ __device__ __forceinline__ void read_w_group(const uint8_t* slot, uint32_t (&W)[
 constexpr int kVWK = 1;      // producer ships W+K (consumer: one VOP2 add)
 constexpr int kVRtSlot = 2;  // slot address computed at run time
 constexpr int kVUnmask = 4;  // unmasked commit while every lane is live
-// Measured on MI355X (profiles/split_variants_r01.json, 4096..32768
-// chunks): with 3-block units the W+K hand-off costs more on the producer
-// side than it saves in the consumer and the run-time slot address is
-// faster; with 2-block units W+K wins (by ~5%) and the slot form does not
-// matter.  Unmasked commit helps both.
+// Diagnostic-only bits (timing experiments; digests are wrong by design and
+// AUTO never selects them; reachable only through SHA1CHUNK_SPLIT_UNIT):
+constexpr int kVDiagNoRead = 8;    // consumer never reads the schedule from LDS
+constexpr int kVDiagIdleProd = 16;  // producer only keeps the barrier count
+constexpr int kVDiagIdleCons = 32;  // consumer only keeps the barrier count
+// Why W+K matters: the consumer's x = e + W + K as a VOP3 v_add3 (K in an
+// SGPR or a VGPR alike) runs the one-wave round stream at ~4.98 cycles per
+// instruction, the VOP2 v_add on a shipped W+K at the 4-cycle issue floor
+// (tools/consumer_probe, profiles/issue_r01.json).  With ONE producer the
+// extra 80 adds per block make the producer the slower wave (1878 vs 1757
+// cycles per block), so single-producer kernels with 3- and 4-block units
+// keep K in the consumer; the 4-block default has TWO producers (kSplitNProd)
+// and ships W+K.  Measured on MI355X (profiles/split_variants_r01.json):
+// 2-block units W+K ~5% ahead, the slot-address form neutral there; unmasked
+// commit helps every shape.
 template <int U>
-constexpr int kSplitV = U >= 3 ? (kVRtSlot | kVUnmask) : (kVWK | kVUnmask);
+constexpr int kSplitV = U == 4 ? (kVWK | kVUnmask) : U == 3 ? (kVRtSlot | kVUnmask) : (kVWK | kVUnmask);
+template <int U>
+constexpr int kSplitNProd = U == 4 ? 2 : 1;
 
 template <int U, int J, int V, bool MASK>
 __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (&h)[5],
@@ -305,20 +322,21 @@ __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (
         slot = ring + slot_idx * kWBlockBytes + lane * 16;
     }
     if constexpr (jn == 0) split_barrier();
+    constexpr bool RD = (V & kVDiagNoRead) == 0;
     uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
-    read_w_group<0>(slot, Wn);
+    if constexpr (RD) read_w_group<0>(slot, Wn);
     __builtin_amdgcn_sched_barrier(0);
     RoundsW<0, 20, WK>::run(v, Wc);
     __builtin_amdgcn_sched_barrier(0);
-    read_w_group<1>(slot, Wn);
+    if constexpr (RD) read_w_group<1>(slot, Wn);
     __builtin_amdgcn_sched_barrier(0);
     RoundsW<20, 40, WK>::run(v, Wc);
     __builtin_amdgcn_sched_barrier(0);
-    read_w_group<2>(slot, Wn);
+    if constexpr (RD) read_w_group<2>(slot, Wn);
     __builtin_amdgcn_sched_barrier(0);
     RoundsW<40, 60, WK>::run(v, Wc);
     __builtin_amdgcn_sched_barrier(0);
-    read_w_group<3>(slot, Wn);
+    if constexpr (RD) read_w_group<3>(slot, Wn);
     __builtin_amdgcn_sched_barrier(0);
     RoundsW<60, 80, WK>::run(v, Wc);
     if constexpr (MASK) {
@@ -351,14 +369,23 @@ struct ConsumeUnits {
 // SIMD hosts exactly one consumer and its own producer (the consumer keeps
 // the SIMD's issue slots it needs; the producer fills the rest).  All waves
 // share one s_barrier sequence, so the unit count is the workgroup maximum.
-template <int U, int PAIRS, int V = kSplitV<U>>
-__global__ __launch_bounds__(128 * PAIRS) void sha1_split_kernel(BatchArgs A) {
+//
+// NPROD = 2 (one pair, U = 4): wave 0 consumes, waves 1 and 2 produce,
+// each writing one of the unit's two stages.  The producer's schedule work
+// per block (byte swap, 64-word expansion, W+K, 20 ds_write_b128) is then
+// half as long as the consumer's rounds, so the W+K hand-off, whose
+// VOP2-add consumer issues at the 4-cycle floor, is no longer producer-bound
+// (tools/consumer_probe, tools/replay_probe).
+template <int U, int PAIRS, int V = kSplitV<U>, int NPROD = 1>
+__global__ __launch_bounds__(64 * PAIRS * (1 + NPROD)) void sha1_split_kernel(BatchArgs A) {
     constexpr bool WK = (V & kVWK) != 0;
     static_assert(PAIRS * 2 * U * kWBlockBytes <= 160 * 1024, "LDS");
+    static_assert(NPROD == 1 || (PAIRS == 1 && U == 2 * NPROD), "two producers: one stage each per unit");
     __shared__ __attribute__((aligned(16))) uint8_t lds[PAIRS * 2 * U * kWBlockBytes];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int pair = wave % PAIRS;
     const bool producer = wave >= PAIRS;
+    const uint32_t pidx = producer ? (uint32_t)(wave - PAIRS) / PAIRS : 0u;  // producer index
     const int lane = threadIdx.x & 63;
     uint8_t* ring = lds + pair * (2 * U * kWBlockBytes);
     const uint32_t group = blockIdx.x * PAIRS + (uint32_t)pair;
@@ -384,7 +411,10 @@ __global__ __launch_bounds__(128 * PAIRS) void sha1_split_kernel(BatchArgs A) {
     // past a lane's T are computed on stale data and never committed.
     const uint32_t units = (Tmax + 2 * U - 1) / (2 * U) * 2;
 
-    if (producer) {
+    if (producer && (V & kVDiagIdleProd)) {
+        // diagnostic: same barrier sequence as the consumer, no LDS traffic
+        for (uint32_t m = 0; m <= units; ++m) split_barrier();
+    } else if (producer) {
         // ----------------------------- producer -------------------------
         // Bulk: stages (2 full blocks) that every lane has, when every lane's
         // chunk is 16-byte aligned (branch-free loads hipcc can count);
@@ -394,21 +424,34 @@ __global__ __launch_bounds__(128 * PAIRS) void sha1_split_kernel(BatchArgs A) {
                                ? __builtin_amdgcn_readfirstlane(
                                      wave_min(valid ? (en.len >> 7) : 0xffffffffu))
                                : 0u;
+        // this producer's stages: s = pidx, pidx + NPROD, ...
         Stage A0, A1;
-        if (S > 0) load_stage(en.p, A0);
-        if (S > 1) load_stage(en.p + 128, A1);
-        uint32_t s = 0;
-        for (; s + 1 < S; s += 2) {
-            produce_stage<U, WK>(en, s, S, A0, ring, lane);
-            produce_stage<U, WK>(en, s + 1, S, A1, ring, lane);
+        if (pidx < S) load_stage(en.p + 128ull * pidx, A0);
+        if (pidx + NPROD < S) load_stage(en.p + 128ull * (pidx + NPROD), A1);
+        uint32_t s = pidx;
+        for (; s + NPROD < S; s += 2 * NPROD) {
+            produce_stage<U, WK, NPROD>(en, s, S, A0, ring, lane);
+            produce_stage<U, WK, NPROD>(en, s + NPROD, S, A1, ring, lane);
         }
-        if (s < S) produce_stage<U, WK>(en, s, S, A0, ring, lane);
-        for (uint32_t k = 2 * S; k < units * U; ++k) {
-            uint32_t w[16];
-            if (k < T) tail_block_words(en, k, w);
-            produce_block<U, WK>(k, w, ring, lane);
+        if (s < S) {
+            produce_stage<U, WK, NPROD>(en, s, S, A0, ring, lane);
+            s += NPROD;
+        }
+        // tail and padding stages (whole units: blocks past a lane's T are
+        // never committed by the consumer)
+        for (; 2 * s < units * U; s += NPROD) {
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                const uint32_t k = 2 * s + half;
+                uint32_t w[16];
+                if (k < T) tail_block_words(en, k, w);
+                produce_block<U, WK, NPROD>(k, w, ring, lane);
+            }
         }
         split_barrier();  // matches the consumer's last (unused) read
+    } else if (V & kVDiagIdleCons) {
+        // diagnostic: the producer alone sets the pace
+        for (uint32_t m = 0; m <= units; ++m) split_barrier();
     } else {
         // ----------------------------- consumer -------------------------
         uint32_t h[5];
@@ -539,7 +582,10 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     case 1: hipLaunchKernelGGL((sha1_split_kernel<1, 1>), dim3(groups), dim3(128), 0, st, A); break;
     case 2: hipLaunchKernelGGL((sha1_split_kernel<2, 1>), dim3(groups), dim3(128), 0, st, A); break;
     case 3: hipLaunchKernelGGL((sha1_split_kernel<3, 1>), dim3(groups), dim3(128), 0, st, A); break;
-    case 4: hipLaunchKernelGGL((sha1_split_kernel<4, 1>), dim3(groups), dim3(128), 0, st, A); break;
+    case 4:  // two producers per consumer (kSplitNProd<4>): 192 threads
+        hipLaunchKernelGGL((sha1_split_kernel<4, 1, kSplitV<4>, kSplitNProd<4>>), dim3(groups),
+                           dim3(64 * (1 + kSplitNProd<4>)), 0, st, A);
+        break;
 #define SPLIT_V(U, V)                                                                             \
     case 10 * U + V:                                                                              \
         hipLaunchKernelGGL((sha1_split_kernel<U, 1, V>), dim3(groups), dim3(128), 0, st, A);   \
@@ -547,8 +593,22 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     // A/B variants: unit 10*U + V (V = kVWK | kVRtSlot | kVUnmask bits)
     SPLIT_V(3, 0) SPLIT_V(3, 1) SPLIT_V(3, 2) SPLIT_V(3, 3) SPLIT_V(3, 4) SPLIT_V(3, 6)
     SPLIT_V(3, 7) SPLIT_V(2, 0) SPLIT_V(2, 1) SPLIT_V(2, 2) SPLIT_V(2, 3) SPLIT_V(2, 4) SPLIT_V(2, 6)
-    SPLIT_V(2, 7) SPLIT_V(4, 2) SPLIT_V(4, 4) SPLIT_V(4, 5)
+    SPLIT_V(2, 7) SPLIT_V(4, 2) SPLIT_V(4, 4) SPLIT_V(4, 5) SPLIT_V(4, 6)
 #undef SPLIT_V
+#define SPLIT_D(U, V)                                                                             \
+    case 100 * U + V:                                                                             \
+        hipLaunchKernelGGL((sha1_split_kernel<U, 1, V>), dim3(groups), dim3(128), 0, st, A);   \
+        break;
+    // diagnostic timing variants (kVDiag* bits): unit 100*U + V
+    SPLIT_D(4, 14) SPLIT_D(4, 22) SPLIT_D(4, 30) SPLIT_D(4, 37) SPLIT_D(4, 38) SPLIT_D(4, 13)
+#undef SPLIT_D
+#define SPLIT_2P(V)                                                                               \
+    case 500 + V:                                                                                 \
+        hipLaunchKernelGGL((sha1_split_kernel<4, 1, V, 2>), dim3(groups), dim3(192), 0, st, A);   \
+        break;
+    // two producer waves per consumer, 4-block units: unit 500 + V
+    SPLIT_2P(4) SPLIT_2P(5) SPLIT_2P(6) SPLIT_2P(7) SPLIT_2P(37) SPLIT_2P(38)
+#undef SPLIT_2P
     case 8:  // 4 pairs per workgroup (512 threads), one consumer + producer per SIMD
         hipLaunchKernelGGL((sha1_split_kernel<1, 4>), dim3((groups + 3) / 4), dim3(512), 0, st, A);
         break;

@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--out", default=None)
     ap.add_argument("--lib", default=None, help="A/B: load this libsha1chunk.so instead")
+    ap.add_argument("--no-check", action="store_true",
+                    help="timing only: skip the cross-kernel digest check (diagnostic variants)")
     a = ap.parse_args()
     import torch
     pkg = importlib.import_module("congestion-control-with-bittorren_amd")
@@ -60,7 +62,7 @@ def main():
                 d = dig.cpu().numpy()
                 if ref is None:
                     ref = d
-                assert np.array_equal(d, ref), f"kernel {k} disagrees at n={n}"
+                assert a.no_check or np.array_equal(d, ref), f"kernel {k} disagrees at n={n}"
         for k in kernels:
             ms = float(np.median(times[k]))
             row = {"chunks": n, "chunk_bytes": L, "kernel": k, "ms": round(ms, 4),
