@@ -13,7 +13,7 @@ Prints ONE JSON line on rank 0 with `roofline` (dominant kernel vs the HBM
 peak, per-launch time from HIP events on the kernel's own stream; `traffic`
 from the committed rocprofv3 PMC pass, profiles/traffic_*.json),
 `serial_bound` (the per-chunk limit that actually binds this workload: SHA-1
-is serial inside a chunk and one wave issues one instruction per ~4.63
+is serial inside a chunk and one wave issues one instruction per 4
 cycles, so 4096 chunks = 64 waves cannot fill 1024 SIMDs) and
 `cpu_baseline` (the reference sha.c, compiled from its sources into
 oracle/_ref, timed on this host's cores on the same chunks).
@@ -40,15 +40,16 @@ sys.path.insert(0, ROOT)
 METRIC = "GiB/s device-resident SHA-1 over 512KB chunks; % of HBM-read roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 # Per-chunk serial floor: a rounds-only wave needs 5 VALU per round x 80
-# rounds per 64-B block; one wave issues one instruction per 4.63 cycles
-# (measured, tools/microbench.hip -> profiles/microbench_issue_r01.json) at
-# the 2.4 GHz the chip holds at this occupancy.
+# rounds per 64-B block, and one wave issues one instruction per 4.0 cycles
+# (straight-line streams, tools/issue_probe.hip -> profiles/issue_r01.json;
+# looped microbenchmarks read 4.63 because of their loop branch) at the
+# ~2.4 GHz the chip holds at this occupancy.
 ROUND_VALU_PER_BLOCK = 400
 # The split consumer's whole per-block stream (400 round ops + 20 ds_read_b128
-# of the schedule + 5 feed-forward adds + loop/barrier scalars), counted in
-# the unrolled 8-block loop of sha1_split_kernel<4,1> (`make isa`).
+# of the schedule + 5 feed-forward adds + waits/barrier scalars), counted in
+# the unrolled 8-block loop of the 4-block-unit kernel (`make isa`).
 CONSUMER_INSTR_PER_BLOCK = 428
-ISSUE_CYCLES = 4.63
+ISSUE_CYCLES = 4.0
 CLOCK_HZ = 2.4e9
 # VALU-int roofline: the algorithmic SHA-1 op count per 64-B
 # block (80 x 5 round ops + 64 x 3 schedule ops + 16 byte swaps + 5
@@ -195,10 +196,10 @@ def main():
             "bound": "per-chunk serial VALU issue (rounds-only wave)",
             "floor_ms": round(floor_ms, 4), "achieved_ms": round(kern_ms, 4),
             "frac": round(floor_ms / kern_ms, 4),
-            "model": f"{blocks} blocks x {ROUND_VALU_PER_BLOCK} VALU x {ISSUE_CYCLES} cyc / 2.4 GHz",
+            "model": f"{blocks} blocks x {ROUND_VALU_PER_BLOCK} VALU x {ISSUE_CYCLES:g} cyc / 2.4 GHz",
             "stream_floor_ms": round(stream_ms, 4), "stream_frac": round(stream_ms / kern_ms, 4),
             "stream_model": f"{blocks} blocks x {CONSUMER_INSTR_PER_BLOCK} consumer instructions "
-                            f"x {ISSUE_CYCLES} cyc / 2.4 GHz",
+                            f"x {ISSUE_CYCLES:g} cyc / 2.4 GHz",
         },
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
