@@ -222,16 +222,17 @@ __device__ __forceinline__ void tail_block_words(const Entry& en, uint32_t k, ui
     }
 }
 
-// NPROD producer waves share the stages (2 blocks each) of a unit: with
-// NPROD = 2 and U = 4 each producer owns one stage per unit, so it ends
-// every unit with its own barrier after the unit's odd block; a single
-// producer ends the unit after block U-1.
+// NPROD producer waves share a unit's blocks.  NPROD = 2 (U = 4): each
+// producer owns one stage (2 blocks) per unit and ends the unit with its
+// barrier after that stage's odd block.  A single producer ends the unit
+// after block U-1.
 template <int U, bool WK, int NPROD = 1>
 __device__ __forceinline__ void produce_block(uint32_t k, uint32_t (&w)[16], uint8_t* ring, int lane) {
     const uint32_t m = k / U, j = k - m * U;
     SchedWrite<0, WK>::run(w, ring + ((m & 1u) * U + j) * kWBlockBytes, lane);
     if (NPROD == 1 ? j == U - 1 : (k & 1u) == 1u) split_barrier();
 }
+
 
 // Two blocks (128 contiguous bytes) of one lane's chunk, loaded per lane.
 struct Stage {
@@ -380,6 +381,9 @@ template <int U, int PAIRS, int V = kSplitV<U>, int NPROD = 1>
 __global__ __launch_bounds__(64 * PAIRS * (1 + NPROD)) void sha1_split_kernel(BatchArgs A) {
     constexpr bool WK = (V & kVWK) != 0;
     static_assert(PAIRS * 2 * U * kWBlockBytes <= 160 * 1024, "LDS");
+    // Two producers for 2-block units (each owning one block per unit) were
+    // measured slower at two groups per CU: 6 waves on 4 SIMDs put producers
+    // on the consumers' SIMDs (profiles/split_2prod_sweep_r01.json).
     static_assert(NPROD == 1 || (PAIRS == 1 && U == 2 * NPROD), "two producers: one stage each per unit");
     __shared__ __attribute__((aligned(16))) uint8_t lds[PAIRS * 2 * U * kWBlockBytes];
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -609,6 +613,7 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     // two producer waves per consumer, 4-block units: unit 500 + V
     SPLIT_2P(4) SPLIT_2P(5) SPLIT_2P(6) SPLIT_2P(7) SPLIT_2P(37) SPLIT_2P(38)
 #undef SPLIT_2P
+
     case 8:  // 4 pairs per workgroup (512 threads), one consumer + producer per SIMD
         hipLaunchKernelGGL((sha1_split_kernel<1, 4>), dim3((groups + 3) / 4), dim3(512), 0, st, A);
         break;
