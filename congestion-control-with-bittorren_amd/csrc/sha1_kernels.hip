@@ -15,17 +15,20 @@
 //                      (~627 instructions per block), two 128-byte stages of
 //                      each chunk prefetched per lane.  The high-occupancy
 //                      kernel: >= 2 groups of 64 chunks per CU.
-//   sha1_split_kernel  workgroup = producer wave + consumer wave on the same
-//                      64 chunks.  The producer streams and byte-swaps the
-//                      blocks and expands the 80-word schedule into an LDS
-//                      ring; the consumer runs only the 80 rounds (~438
+//   sha1_split_kernel  workgroup = consumer wave + producer wave(s) on the
+//                      same 64 chunks.  Producers stream and byte-swap the
+//                      blocks and expand the 80-word schedule (+K) into an
+//                      LDS ring; the consumer runs only the 80 rounds (~428
 //                      instructions per block instead of ~627), which is the
 //                      bound when there are too few chunks to fill the
 //                      SIMDs (BASELINE config 2: 4096 chunks = 64 waves).
 //
-// Measured on MI355X (tools/microbench.hip): one wave issues at
-// most one instruction per ~4.63 cycles; v_alignbit/v_add3/v_perm cost ~1.9
-// ns of SIMD time per wave-instruction vs ~1.1 ns for v_add/v_xor/v_bitop3.
+// Measured on MI355X (tools/issue_probe.hip, tools/gen_consumer_probe.py,
+// DESIGN.md section 5): one wave issues at most one instruction per 4.0
+// cycles; its round stream reaches that with x = e + (W+K) as a VOP2 add and
+// runs at ~5 cycles per VALU with a VOP3 add3 of K; at several waves per SIMD
+// v_alignbit/v_add3/v_perm cost ~1.9 ns of SIMD time per wave-instruction vs
+// ~1.1 ns for v_add/v_xor/v_bitop3.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
