@@ -287,11 +287,10 @@ __device__ __forceinline__ void read_w_group(const uint8_t* slot, uint32_t (&W)[
 constexpr int kVWK = 1;      // producer ships W+K (consumer: one VOP2 add)
 constexpr int kVRtSlot = 2;  // slot address computed at run time
 constexpr int kVUnmask = 4;  // unmasked commit while every lane is live
-// Diagnostic-only bits (timing experiments; digests are wrong by design and
-// AUTO never selects them; reachable only through SHA1CHUNK_SPLIT_UNIT):
-constexpr int kVDiagNoRead = 8;    // consumer never reads the schedule from LDS
-constexpr int kVDiagIdleProd = 16;  // producer only keeps the barrier count
-constexpr int kVDiagIdleCons = 32;  // consumer only keeps the barrier count
+// (The timing study behind these defaults also used variants in which the
+// consumer skipped its LDS reads or one side idled at the barriers; their
+// digests are wrong by design, so they are not built into the library.
+// Results: profiles/issue_r01.json, profiles/split_2prod_sweep_r01.json.)
 // With two producers, launch 4 waves and leave wave 2 empty, so both
 // producers (waves 1, 3) sit on the other LDS store-path half than the
 // consumer (a workgroup's waves alternate halves, SIMDs {0,1} / {2,3}):
@@ -332,21 +331,20 @@ __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (
         slot = ring + slot_idx * kWBlockBytes + lane * 16;
     }
     if constexpr (jn == 0) split_barrier();
-    constexpr bool RD = (V & kVDiagNoRead) == 0;
     uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
-    if constexpr (RD) read_w_group<0>(slot, Wn);
+    read_w_group<0>(slot, Wn);
     __builtin_amdgcn_sched_barrier(0);
     RoundsW<0, 20, WK>::run(v, Wc);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (RD) read_w_group<1>(slot, Wn);
+    read_w_group<1>(slot, Wn);
     __builtin_amdgcn_sched_barrier(0);
     RoundsW<20, 40, WK>::run(v, Wc);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (RD) read_w_group<2>(slot, Wn);
+    read_w_group<2>(slot, Wn);
     __builtin_amdgcn_sched_barrier(0);
     RoundsW<40, 60, WK>::run(v, Wc);
     __builtin_amdgcn_sched_barrier(0);
-    if constexpr (RD) read_w_group<3>(slot, Wn);
+    read_w_group<3>(slot, Wn);
     __builtin_amdgcn_sched_barrier(0);
     RoundsW<60, 80, WK>::run(v, Wc);
     if constexpr (MASK) {
@@ -430,10 +428,7 @@ __global__ __launch_bounds__(64 * PAIRS * (1 + NPROD) + ((V & kVSkipWave2) ? 64 
     // past a lane's T are computed on stale data and never committed.
     const uint32_t units = (Tmax + 2 * U - 1) / (2 * U) * 2;
 
-    if (producer && (V & kVDiagIdleProd)) {
-        // diagnostic: same barrier sequence as the consumer, no LDS traffic
-        for (uint32_t m = 0; m <= units; ++m) split_barrier();
-    } else if (producer) {
+    if (producer) {
         // ----------------------------- producer -------------------------
         // Bulk: stages (2 full blocks) that every lane has, when every lane's
         // chunk is 16-byte aligned (branch-free loads hipcc can count);
@@ -468,9 +463,6 @@ __global__ __launch_bounds__(64 * PAIRS * (1 + NPROD) + ((V & kVSkipWave2) ? 64 
             }
         }
         split_barrier();  // matches the consumer's last (unused) read
-    } else if (V & kVDiagIdleCons) {
-        // diagnostic: the producer alone sets the pace
-        for (uint32_t m = 0; m <= units; ++m) split_barrier();
     } else {
         // ----------------------------- consumer -------------------------
         uint32_t h[5];
@@ -615,19 +607,12 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     SPLIT_V(3, 7) SPLIT_V(2, 0) SPLIT_V(2, 1) SPLIT_V(2, 2) SPLIT_V(2, 3) SPLIT_V(2, 4) SPLIT_V(2, 6)
     SPLIT_V(2, 7) SPLIT_V(4, 2) SPLIT_V(4, 4) SPLIT_V(4, 5) SPLIT_V(4, 6)
 #undef SPLIT_V
-#define SPLIT_D(U, V)                                                                             \
-    case 100 * U + V:                                                                             \
-        hipLaunchKernelGGL((sha1_split_kernel<U, 1, V>), dim3(groups), dim3(128), 0, st, A);   \
-        break;
-    // diagnostic timing variants (kVDiag* bits): unit 100*U + V
-    SPLIT_D(4, 14) SPLIT_D(4, 22) SPLIT_D(4, 30) SPLIT_D(4, 37) SPLIT_D(4, 38) SPLIT_D(4, 13)
-#undef SPLIT_D
 #define SPLIT_2P(V)                                                                               \
     case 500 + V:                                                                                 \
         hipLaunchKernelGGL((sha1_split_kernel<4, 1, V, 2>), dim3(groups), dim3(192), 0, st, A);   \
         break;
     // two producer waves per consumer, 4-block units: unit 500 + V
-    SPLIT_2P(4) SPLIT_2P(5) SPLIT_2P(6) SPLIT_2P(7) SPLIT_2P(37) SPLIT_2P(38) SPLIT_2P(21) SPLIT_2P(13)
+    SPLIT_2P(4) SPLIT_2P(5) SPLIT_2P(6) SPLIT_2P(7)
 #undef SPLIT_2P
     case 569:  // 500 + (kVWK | kVUnmask | kVSkipWave2): producers on waves 1 and 3
         hipLaunchKernelGGL((sha1_split_kernel<4, 1, 69, 2>), dim3(groups), dim3(256), 0, st, A);

@@ -228,12 +228,14 @@ int choose_kernel(int kernel, size_t n, int cus) {
 
 // Split-kernel shape: 4-block units (1 barrier per 4 blocks, the whole 160
 // KiB LDS) at one workgroup per CU, 2-block units (80 KiB) at two per CU,
-// else 1-block units (40 KiB).  SHA1CHUNK_SPLIT_UNIT overrides (1..4 units,
-// 8/9 multi-pair shapes, 10*U+V variants; see launch_split).
+// else 1-block units (40 KiB).  SHA1CHUNK_SPLIT_UNIT overrides for A/B runs
+// (1..4 units, 8/9 multi-pair shapes, 10*U+V single-producer variants,
+// 500+V / 569 two-producer 4-block variants; see launch_split).
 int split_unit(size_t n, int cus) {
     if (const char* e = getenv("SHA1CHUNK_SPLIT_UNIT")) {
         const int u = atoi(e);
-        if ((u >= 1 && u <= 4) || u == 8 || u == 9 || (u >= 20 && u <= 47) || (u >= 400 && u <= 463) || (u >= 500 && u <= 569))
+        if ((u >= 1 && u <= 4) || u == 8 || u == 9 || (u >= 20 && u <= 47) || (u >= 500 && u <= 507) ||
+            u == 569)
             return u;
     }
     const size_t groups = (n + 63) / 64;
