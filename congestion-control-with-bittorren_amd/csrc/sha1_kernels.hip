@@ -287,6 +287,7 @@ __device__ __forceinline__ void read_w_group(const uint8_t* slot, uint32_t (&W)[
 constexpr int kVWK = 1;      // producer ships W+K (consumer: one VOP2 add)
 constexpr int kVRtSlot = 2;  // slot address computed at run time
 constexpr int kVUnmask = 4;  // unmasked commit while every lane is live
+constexpr int kVRead10 = 8;  // schedule reads in two bursts of 10 instead of four of 5
 // (The timing study behind these defaults also used variants in which the
 // consumer skipped its LDS reads or one side idled at the barriers; their
 // digests are wrong by design, so they are not built into the library.
@@ -307,7 +308,7 @@ constexpr int kVSkipWave2 = 64;
 // 2-block units W+K ~5% ahead, the slot-address form neutral there; unmasked
 // commit helps every shape.
 template <int U>
-constexpr int kSplitV = U == 4 ? (kVWK | kVUnmask | kVSkipWave2)
+constexpr int kSplitV = U == 4 ? (kVWK | kVUnmask | kVSkipWave2 | kVRead10)
                                : U == 3 ? (kVRtSlot | kVUnmask) : (kVWK | kVUnmask);
 template <int U>
 constexpr int kSplitNProd = U == 4 ? 2 : 1;
@@ -332,21 +333,34 @@ __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (
     }
     if constexpr (jn == 0) split_barrier();
     uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
-    read_w_group<0>(slot, Wn);
-    __builtin_amdgcn_sched_barrier(0);
-    RoundsW<0, 20, WK>::run(v, Wc);
-    __builtin_amdgcn_sched_barrier(0);
-    read_w_group<1>(slot, Wn);
-    __builtin_amdgcn_sched_barrier(0);
-    RoundsW<20, 40, WK>::run(v, Wc);
-    __builtin_amdgcn_sched_barrier(0);
-    read_w_group<2>(slot, Wn);
-    __builtin_amdgcn_sched_barrier(0);
-    RoundsW<40, 60, WK>::run(v, Wc);
-    __builtin_amdgcn_sched_barrier(0);
-    read_w_group<3>(slot, Wn);
-    __builtin_amdgcn_sched_barrier(0);
-    RoundsW<60, 80, WK>::run(v, Wc);
+    if constexpr ((V & kVRead10) != 0) {
+        // two bursts of 10 reads (before rounds 0 and 40)
+        read_w_group<0>(slot, Wn);
+        read_w_group<1>(slot, Wn);
+        __builtin_amdgcn_sched_barrier(0);
+        RoundsW<0, 40, WK>::run(v, Wc);
+        __builtin_amdgcn_sched_barrier(0);
+        read_w_group<2>(slot, Wn);
+        read_w_group<3>(slot, Wn);
+        __builtin_amdgcn_sched_barrier(0);
+        RoundsW<40, 80, WK>::run(v, Wc);
+    } else {
+        read_w_group<0>(slot, Wn);
+        __builtin_amdgcn_sched_barrier(0);
+        RoundsW<0, 20, WK>::run(v, Wc);
+        __builtin_amdgcn_sched_barrier(0);
+        read_w_group<1>(slot, Wn);
+        __builtin_amdgcn_sched_barrier(0);
+        RoundsW<20, 40, WK>::run(v, Wc);
+        __builtin_amdgcn_sched_barrier(0);
+        read_w_group<2>(slot, Wn);
+        __builtin_amdgcn_sched_barrier(0);
+        RoundsW<40, 60, WK>::run(v, Wc);
+        __builtin_amdgcn_sched_barrier(0);
+        read_w_group<3>(slot, Wn);
+        __builtin_amdgcn_sched_barrier(0);
+        RoundsW<60, 80, WK>::run(v, Wc);
+    }
     if constexpr (MASK) {
         const bool live = k < T;
 #pragma unroll
@@ -616,6 +630,9 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
 #undef SPLIT_2P
     case 569:  // 500 + (kVWK | kVUnmask | kVSkipWave2): producers on waves 1 and 3
         hipLaunchKernelGGL((sha1_split_kernel<4, 1, 69, 2>), dim3(groups), dim3(256), 0, st, A);
+        break;
+    case 577:  // 569 + kVRead10
+        hipLaunchKernelGGL((sha1_split_kernel<4, 1, 77, 2>), dim3(groups), dim3(256), 0, st, A);
         break;
 
     case 8:  // 4 pairs per workgroup (512 threads), one consumer + producer per SIMD
