@@ -227,13 +227,15 @@ __device__ __forceinline__ void tail_block_words(const Entry& en, uint32_t k, ui
 
 // NPROD producer waves share a unit's blocks.  NPROD = 2 (U = 4): each
 // producer owns one stage (2 blocks) per unit and ends the unit with its
-// barrier after that stage's odd block.  A single producer ends the unit
-// after block U-1.
+// barrier after that stage's odd block.  NPROD = U = 2: each producer owns
+// one block per unit and ends the unit after it.  A single producer ends the
+// unit after block U-1.
 template <int U, bool WK, int NPROD = 1>
 __device__ __forceinline__ void produce_block(uint32_t k, uint32_t (&w)[16], uint8_t* ring, int lane) {
     const uint32_t m = k / U, j = k - m * U;
     SchedWrite<0, WK>::run(w, ring + ((m & 1u) * U + j) * kWBlockBytes, lane);
-    if (NPROD == 1 ? j == U - 1 : (k & 1u) == 1u) split_barrier();
+    // U == NPROD: each producer writes one block of every unit
+    if (NPROD == 1 ? j == U - 1 : (U == NPROD || (k & 1u) == 1u)) split_barrier();
 }
 
 
@@ -268,6 +270,18 @@ __device__ __forceinline__ void produce_stage(const Entry& en, uint32_t s, uint3
     }
 }
 
+// Producer that owns one block per unit (U == NPROD): block k from `cur`,
+// which is then refilled with this producer's block after next, k + 2 NPROD.
+template <int U, bool WK, int NPROD>
+__device__ __forceinline__ void produce_own_block(const Entry& en, uint32_t k, uint32_t K,
+                                                  uint32_t (&cur)[16], uint8_t* ring, int lane) {
+    uint32_t w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = bswap(cur[j]);
+    if (k + 2 * NPROD < K) load_block_a16(en.p + 64ull * (k + 2 * NPROD), cur);
+    produce_block<U, WK, NPROD>(k, w, ring, lane);
+}
+
 template <int P>
 __device__ __forceinline__ void read_w_group(const uint8_t* slot, uint32_t (&W)[80]) {
 #pragma unroll
@@ -297,6 +311,17 @@ constexpr int kVRead10 = 8;  // schedule reads in two bursts of 10 instead of fo
 // consumer (a workgroup's waves alternate halves, SIMDs {0,1} / {2,3}):
 // measured 2-3% faster than 3 waves (profiles/split_2prod_sweep_r01.json).
 constexpr int kVSkipWave2 = 64;
+// Two pairs per workgroup with two producers each, 2-block units (one
+// block per producer per unit), 8 waves: a workgroup's waves w and w + 4
+// share a SIMD and waves 0-3 sit on four different SIMDs
+// (tools/wave_placement_probe), so the consumers go on waves 0 and 2 with
+// waves 4 and 6 left empty (each consumer alone on its SIMD), and each
+// pair's producers share one of the other two SIMDs: waves 1 + 5 and 3 + 7.
+// kVCross swaps which producer SIMD serves which consumer.
+constexpr int kVLayout8 = 128;
+constexpr int kVCross = 256;
+template <int PAIRS, int V, int NPROD>
+constexpr int kSplitThreads = (V & kVLayout8) ? 512 : 64 * PAIRS * (1 + NPROD) + ((V & kVSkipWave2) ? 64 : 0);
 // Why W+K matters: the consumer's x = e + W + K as a VOP3 v_add3 (K in an
 // SGPR or a VGPR alike) runs the one-wave round stream at ~4.98 cycles per
 // instruction, the VOP2 v_add on a shipped W+K at the 4-cycle issue floor
@@ -399,14 +424,16 @@ struct ConsumeUnits {
 // VOP2-add consumer issues at the 4-cycle floor, is no longer producer-bound
 // (tools/consumer_probe, tools/replay_probe).
 template <int U, int PAIRS, int V = kSplitV<U>, int NPROD = 1>
-__global__ __launch_bounds__(64 * PAIRS * (1 + NPROD) + ((V & kVSkipWave2) ? 64 : 0)) void sha1_split_kernel(
+__global__ __launch_bounds__((kSplitThreads<PAIRS, V, NPROD>)) void sha1_split_kernel(
     BatchArgs A) {
     constexpr bool WK = (V & kVWK) != 0;
     static_assert(PAIRS * 2 * U * kWBlockBytes <= 160 * 1024, "LDS");
     // Two producers for 2-block units (each owning one block per unit) were
     // measured slower at two groups per CU: 6 waves on 4 SIMDs put producers
     // on the consumers' SIMDs (profiles/split_2prod_sweep_r01.json).
-    static_assert(NPROD == 1 || (PAIRS == 1 && U == 2 * NPROD), "two producers: one stage each per unit");
+    static_assert(NPROD == 1 || (PAIRS == 1 && U == 2 * NPROD) ||
+                      (PAIRS == 2 && U == NPROD && (V & kVLayout8) != 0),
+                  "two producers: one stage (U = 4) or one block (U = 2, 8-wave layout) each per unit");
     __shared__ __attribute__((aligned(16))) uint8_t lds[PAIRS * 2 * U * kWBlockBytes];
     int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if constexpr ((V & kVSkipWave2) != 0) {
@@ -414,9 +441,16 @@ __global__ __launch_bounds__(64 * PAIRS * (1 + NPROD) + ((V & kVSkipWave2) ? 64 
         if (wave == 2) return;  // never joins a barrier: an ended wave is not waited for
         if (wave == 3) wave = 2;
     }
-    const int pair = wave % PAIRS;
-    const bool producer = wave >= PAIRS;
-    const uint32_t pidx = producer ? (uint32_t)(wave - PAIRS) / PAIRS : 0u;  // producer index
+    int pair = wave % PAIRS;
+    bool producer = wave >= PAIRS;
+    uint32_t pidx = producer ? (uint32_t)(wave - PAIRS) / PAIRS : 0u;  // producer index
+    if constexpr ((V & kVLayout8) != 0) {
+        static_assert(PAIRS == 2 && NPROD == 2, "8-wave layout: two pairs, two producers each");
+        if (wave == 4 || wave == 6) return;  // never joins a barrier
+        producer = (wave & 1) != 0;
+        pair = producer ? (((wave >> 1) & 1) ^ ((V & kVCross) ? 1 : 0)) : (wave >> 1);
+        pidx = producer ? (uint32_t)(wave >> 2) : 0u;
+    }
     const int lane = threadIdx.x & 63;
     uint8_t* ring = lds + pair * (2 * U * kWBlockBytes);
     const uint32_t group = blockIdx.x * PAIRS + (uint32_t)pair;
@@ -452,6 +486,30 @@ __global__ __launch_bounds__(64 * PAIRS * (1 + NPROD) + ((V & kVSkipWave2) ? 64 
                                ? __builtin_amdgcn_readfirstlane(
                                      wave_min(valid ? (en.len >> 7) : 0xffffffffu))
                                : 0u;
+        if constexpr (U == NPROD) {
+            // this producer's blocks: k = pidx, pidx + NPROD, ... (one per unit);
+            // bulk over the full blocks every lane has, then tail/padding
+            const uint32_t K = S * 2u;
+            uint32_t B0[16], B1[16];
+            if (pidx < K) load_block_a16(en.p + 64ull * pidx, B0);
+            if (pidx + NPROD < K) load_block_a16(en.p + 64ull * (pidx + NPROD), B1);
+            uint32_t k = pidx;
+            for (; k + NPROD < K; k += 2 * NPROD) {
+                produce_own_block<U, WK, NPROD>(en, k, K, B0, ring, lane);
+                produce_own_block<U, WK, NPROD>(en, k + NPROD, K, B1, ring, lane);
+            }
+            if (k < K) {
+                produce_own_block<U, WK, NPROD>(en, k, K, B0, ring, lane);
+                k += NPROD;
+            }
+            for (; k < units * U; k += NPROD) {
+                uint32_t w[16];
+                if (k < T) tail_block_words(en, k, w);
+                produce_block<U, WK, NPROD>(k, w, ring, lane);
+            }
+            split_barrier();  // matches the consumer's last (unused) read
+            return;
+        }
         // this producer's stages: s = pidx, pidx + NPROD, ...
         Stage A0, A1;
         if (pidx < S) load_stage(en.p + 128ull * pidx, A0);
@@ -637,6 +695,18 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
 
     case 8:  // 4 pairs per workgroup (512 threads), one consumer + producer per SIMD
         hipLaunchKernelGGL((sha1_split_kernel<1, 4>), dim3((groups + 3) / 4), dim3(512), 0, st, A);
+        break;
+    case 10:  // 2 pairs x (consumer + 2 producers), 2-block units, 8-wave layout
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, kVWK | kVUnmask | kVLayout8, 2>), dim3((groups + 1) / 2),
+                           dim3(512), 0, st, A);
+        break;
+    case 11:  // case 10 with the producer SIMDs swapped between the pairs
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, kVWK | kVUnmask | kVLayout8 | kVCross, 2>),
+                           dim3((groups + 1) / 2), dim3(512), 0, st, A);
+        break;
+    case 12:  // case 10 with schedule reads in bursts of 10
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, kVWK | kVUnmask | kVLayout8 | kVRead10, 2>),
+                           dim3((groups + 1) / 2), dim3(512), 0, st, A);
         break;
     case 9:  // 2 pairs per workgroup, 2-block units
         hipLaunchKernelGGL((sha1_split_kernel<2, 2>), dim3((groups + 1) / 2), dim3(256), 0, st, A);

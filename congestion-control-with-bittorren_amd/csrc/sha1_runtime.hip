@@ -227,20 +227,24 @@ int choose_kernel(int kernel, size_t n, int cus) {
 }
 
 // Split-kernel shape: 4-block units (1 barrier per 4 blocks, the whole 160
-// KiB LDS) at one workgroup per CU, 2-block units (80 KiB) at two per CU,
+// KiB LDS, two producers) at one group of 64 chunks per CU; at two groups per
+// CU one 8-wave workgroup holding both, 2-block units, two producers per
+// consumer sharing a SIMD and each consumer alone on its own (case 11:
+// 10-11 % faster than two 2-wave workgroups, profiles/split_2prod_sweep_r01.json);
 // else 1-block units (40 KiB).  SHA1CHUNK_SPLIT_UNIT overrides for A/B runs
 // (1..4 units, 8/9 multi-pair shapes, 10*U+V single-producer variants,
-// 500+V / 569 two-producer 4-block variants; see launch_split).
+// 500+V / 569 / 577 two-producer 4-block variants, 10-12 two pairs with two
+// producers each; see launch_split).
 int split_unit(size_t n, int cus) {
     if (const char* e = getenv("SHA1CHUNK_SPLIT_UNIT")) {
         const int u = atoi(e);
-        if ((u >= 1 && u <= 4) || u == 8 || u == 9 || (u >= 20 && u <= 47) || (u >= 500 && u <= 507) ||
+        if ((u >= 1 && u <= 4) || (u >= 8 && u <= 12) || (u >= 20 && u <= 47) || (u >= 500 && u <= 507) ||
             u == 569 || u == 577)
             return u;
     }
     const size_t groups = (n + 63) / 64;
     if (groups <= size_t(cus)) return 4;
-    if (groups <= size_t(cus) * 2) return 2;
+    if (groups <= size_t(cus) * 2) return 11;
     return 1;
 }
 

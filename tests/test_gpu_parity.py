@@ -547,3 +547,34 @@ def test_make_chunks_from_stream_position(pkg, dev, golden, fixture_files, tmp_p
     exp = [hashlib.sha1(data[i:i + L512]).hexdigest() for i in range(0, len(data), L512)]
     out = subprocess.run([str(exe), str(p), "1000"], capture_output=True, text=True, check=True).stdout
     assert out == "".join(f"{i} {h}\n" for i, h in enumerate(exp)) + "eof 1\n"
+
+
+@pytest.mark.parametrize("unit", [1, 2, 3, 4, 8, 9, 10, 11, 12, 505, 569, 577])
+def test_every_split_shape_ragged(pkg, dev, oracle, unit, monkeypatch):
+    """Every split-kernel shape the library builds (SHA1CHUNK_SPLIT_UNIT
+    forces it: unit sizes, multi-pair workgroups, two-producer layouts) on
+    ragged lengths with byte-misaligned starts, a partial last workgroup and
+    a lane-count that is not a multiple of 64: bit-exact vs the oracle."""
+    torch = dev
+    monkeypatch.setenv("SHA1CHUNK_SPLIT_UNIT", str(unit))
+    rng = np.random.default_rng(1000 + unit)
+    n = 333
+    lens = rng.integers(0, 40000, n).astype(np.uint32)
+    lens[:140] = 65536 + rng.integers(0, 130, 140)   # two waves of long chunks
+    lens[5] = 0
+    lens[6], lens[7], lens[8] = 55, 56, 64
+    for aligned in (True, False):
+        # aligned: every start on a 64-byte boundary (the bulk 16-byte load path)
+        step = ((lens.astype(np.uint64) + 63) // 64 * 64 + 64 if aligned
+                else lens.astype(np.uint64) + rng.integers(1, 40, n).astype(np.uint64))
+        off = np.zeros(n, np.uint64)
+        off[1:] = np.cumsum(step)[: n - 1]
+        host = rng.integers(0, 256, int(off[-1] + lens[-1]) + 64, dtype=np.uint8)
+        want = oracle.hash_batch(host, off, lens)
+        d_dig = torch.zeros((n, 20), dtype=torch.uint8, device="cuda")
+        pkg.hash_device(torch.from_numpy(host).cuda(), torch.from_numpy(off.astype(np.int64)).cuda(),
+                        torch.from_numpy(lens.astype(np.int32)).cuda(), d_dig, kernel="split")
+        torch.cuda.synchronize()
+        got = d_dig.cpu().numpy()
+        bad = np.nonzero((got != want).any(axis=1))[0]
+        assert bad.size == 0, f"unit {unit} aligned={aligned}: {bad.size} bad, first {bad[:8]}"
