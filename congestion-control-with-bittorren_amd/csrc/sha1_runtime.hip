@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cerrno>
 #include <cstdarg>
 #include <cstdio>
@@ -898,12 +899,118 @@ int sha1chunk_synth_fill_ragged_async(void* d_base, const uint64_t* d_offsets,
 }  // extern "C"
 
 // ------------------------------------------------------------ verify queue --
-// Two fill/flight sets per queue: while one set's batch is hashed and
-// compared on the device, submissions fill the other.  Set layout (pinned
-// host and device alike): [off u64 x B][len u32 x B][expected 20 x B] pad to
-// 128 | B slots of `stride` bytes; the device side adds B x 20 digests and
-// B mismatch bytes.
+// Three fill/flight sets per queue: while earlier sets' batches are copied
+// to the device, hashed and compared, submissions fill the next one.  With
+// two, a batch of 1024 chunks had to wait for its set's H2D + kernel (~15
+// ms) and the queue topped out near 30 GiB/s (profiles/file_vq_r01.json).
+// Set layout (pinned host and device alike): [off u64 x B][len u32 x B]
+// [expected 20 x B] pad to 128 | B slots of `stride` bytes; the device side
+// adds B x 20 digests and B mismatch bytes.
 namespace {
+constexpr int kVqSets = 3;
+
+// Helper threads that split one large host copy (a submitted 512 KiB chunk
+// into pinned staging) so that the copy, not one core's memcpy rate
+// (~10-20 GB/s), bounds the queue.  copy() returns when every byte is
+// written, so the caller may reuse its buffer as with one memcpy.
+class CopyPool {
+public:
+    explicit CopyPool(int helpers) {
+        for (int i = 0; i < helpers; ++i) th_.emplace_back([this] { run(); });
+    }
+    ~CopyPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_.store(true);
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    void copy(uint8_t* dst, const uint8_t* src, size_t n) {
+        const size_t parts = std::min<size_t>(th_.size() + 1, n / kMinPiece);
+        if (parts <= 1) {
+            memcpy(dst, src, n);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            dst_ = dst;
+            src_ = src;
+            n_ = n;
+            parts_.store(parts);
+            left_.store(static_cast<int>(parts));
+            next_.store(0);
+            gen_.fetch_add(1);
+        }
+        // helpers still spinning from the previous copy see gen_ at once;
+        // only sleeping ones need the (syscall) wake-up
+        if (sleepers_.load() > 0) cv_.notify_all();
+        work();
+        // the caller's own pieces are done; wait for the helpers' pieces
+        for (int spin = 0; left_.load() != 0 && spin < 200000; ++spin) __builtin_ia32_pause();
+        if (left_.load() != 0) {
+            std::unique_lock<std::mutex> g(mu_);
+            done_.wait(g, [this] { return left_.load() == 0; });
+        }
+    }
+
+private:
+    static constexpr size_t kMinPiece = size_t(64) << 10;
+    // A helper keeps polling for the next copy this many pause loops (tens of
+    // microseconds: a submitter streaming chunks comes back sooner) before it
+    // sleeps on the condition variable.
+    static constexpr int kSpin = 20000;
+    void work() {
+        for (size_t i; (i = next_.fetch_add(1)) < parts_.load();) {
+            const size_t P = parts_.load(), a = n_ * i / P, b = n_ * (i + 1) / P;
+            memcpy(dst_ + a, src_ + a, b - a);
+            if (left_.fetch_sub(1) == 1) {
+                std::lock_guard<std::mutex> g(mu_);
+                done_.notify_all();
+            }
+        }
+    }
+    void run() {
+        uint64_t seen = 0;
+        for (;;) {
+            int spin = 0;
+            while (gen_.load() == seen && !stop_.load() && spin++ < kSpin) __builtin_ia32_pause();
+            if (gen_.load() == seen && !stop_.load()) {
+                std::unique_lock<std::mutex> g(mu_);
+                sleepers_.fetch_add(1);
+                cv_.wait(g, [&] { return stop_.load() || gen_.load() != seen; });
+                sleepers_.fetch_sub(1);
+            }
+            if (stop_.load()) return;
+            {
+                // fields of generation gen_ are published under mu_
+                std::lock_guard<std::mutex> g(mu_);
+                seen = gen_.load();
+            }
+            work();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<int> sleepers_{0};
+    std::atomic<bool> stop_{false};
+    uint8_t* dst_ = nullptr;
+    const uint8_t* src_ = nullptr;
+    size_t n_ = 0;
+    std::atomic<size_t> parts_{0};
+    std::atomic<size_t> next_{0};
+    std::atomic<int> left_{0};
+};
+
+int vq_copy_helpers() {
+    const char* e = getenv("SHA1CHUNK_VQ_THREADS");
+    // threads in all, the caller included; 4 measured best on the GPU box
+    // (16384 x 512 KiB, batch 1024: 1 / 4 / 8 threads 16.9 / 46.4 / 36.5 GiB/s)
+    return std::max(0, (e ? atoi(e) : 4) - 1);
+}
+
 struct VqSet {
     PinBuf h;
     DevBuf d;
@@ -922,11 +1029,12 @@ struct sha1chunk_vq {
     size_t batch = 0;
     uint32_t maxlen = 0;
     size_t stride = 0, meta = 0;
-    VqSet set[2];
+    VqSet set[kVqSets];
     int fill = 0;
     std::deque<int> flight;  // launched sets, oldest first
     std::deque<std::pair<uint64_t, uint8_t>> ready;
     size_t pending = 0;
+    CopyPool* copier = nullptr;
 };
 
 namespace {
@@ -996,6 +1104,7 @@ sha1chunk_vq* sha1chunk_vq_create(size_t batch, uint32_t max_chunk_len) {
     q->maxlen = max_chunk_len;
     q->stride = round_up(max_chunk_len, kAlign);
     q->meta = round_up(batch * (8 + 4 + 20), kAlign);
+    q->copier = new CopyPool(vq_copy_helpers());
     const size_t hbytes = q->meta + batch * q->stride;
     for (auto& S : q->set) {
         if (S.h.ensure(hbytes) || S.d.ensure(hbytes + batch * 21) || S.res.ensure(batch) ||
@@ -1024,14 +1133,14 @@ int sha1chunk_vq_submit(sha1chunk_vq* q, const void* chunk, uint32_t len, const 
     vq_off(q, h)[i] = q->meta + i * q->stride;
     vq_len(q, h)[i] = len;
     memcpy(vq_exp(q, h) + 20 * i, expected, 20);
-    if (len) memcpy(h + q->meta + i * q->stride, chunk, len);
+    if (len) q->copier->copy(h + q->meta + i * q->stride, static_cast<const uint8_t*>(chunk), len);
     S->tags.push_back(tag);
     ++S->count;
     ++q->pending;
     if (S->count == q->batch) {
         int rc = vq_launch(q, q->fill);
         if (rc) return rc;
-        q->fill ^= 1;
+        q->fill = (q->fill + 1) % kVqSets;
     }
     return SHA1CHUNK_OK;
 }
@@ -1041,7 +1150,7 @@ int sha1chunk_vq_flush(sha1chunk_vq* q) {
     if (q->set[q->fill].count == 0 || q->set[q->fill].inflight) return SHA1CHUNK_OK;
     int rc = vq_launch(q, q->fill);
     if (rc) return rc;
-    q->fill ^= 1;
+    q->fill = (q->fill + 1) % kVqSets;
     return SHA1CHUNK_OK;
 }
 
@@ -1084,6 +1193,7 @@ void sha1chunk_vq_destroy(sha1chunk_vq* q) {
         if (S.res.p) (void)hipHostFree(S.res.p);
         if (S.d.p) (void)hipFree(S.d.p);
     }
+    delete q->copier;
     delete q;
 }
 

@@ -123,7 +123,11 @@ int sha1chunk_synth_fill_ragged_async(void *d_base, const uint64_t *d_offsets,
  * every `batch` submissions (or on flush) the batch is hashed and compared on
  * the device asynchronously; poll() returns finished (tag, mismatch) pairs,
  * mismatch following verify_hash: 0 = match, 1 = mismatch -> re-GET.  One
- * queue per thread; queues on one device share nothing. */
+ * queue per thread; queues on one device share nothing.  The copy is split
+ * over SHA1CHUNK_VQ_THREADS threads (default 4, the caller included: three
+ * helper threads per queue that spin briefly between submissions), and three
+ * batch sets are in flight at once, so 1024-chunk batches run near the PCIe
+ * rate. */
 typedef struct sha1chunk_vq sha1chunk_vq;
 /* NULL on failure (sha1chunk_last_error() says why). */
 sha1chunk_vq *sha1chunk_vq_create(size_t batch, uint32_t max_chunk_len);
