@@ -558,12 +558,13 @@ def test_every_split_shape_ragged(pkg, dev, oracle, unit, monkeypatch):
     torch = dev
     monkeypatch.setenv("SHA1CHUNK_SPLIT_UNIT", str(unit))
     rng = np.random.default_rng(1000 + unit)
-    n = 333
-    lens = rng.integers(0, 40000, n).astype(np.uint32)
-    lens[:140] = 65536 + rng.integers(0, 130, 140)   # two waves of long chunks
-    lens[5] = 0
-    lens[6], lens[7], lens[8] = 55, 56, 64
-    for aligned in (True, False):
+    # 333 chunks: 6 groups of 64, the last one partial; 300: 5 groups, so a
+    # two-group workgroup's second group has no valid lane at all
+    for n, aligned in ((333, True), (333, False), (300, True)):
+        lens = rng.integers(0, 40000, n).astype(np.uint32)
+        lens[:140] = 65536 + rng.integers(0, 130, 140)   # two waves of long chunks
+        lens[5] = 0
+        lens[6], lens[7], lens[8] = 55, 56, 64
         # aligned: every start on a 64-byte boundary (the bulk 16-byte load path)
         step = ((lens.astype(np.uint64) + 63) // 64 * 64 + 64 if aligned
                 else lens.astype(np.uint64) + rng.integers(1, 40, n).astype(np.uint64))
@@ -577,4 +578,4 @@ def test_every_split_shape_ragged(pkg, dev, oracle, unit, monkeypatch):
         torch.cuda.synchronize()
         got = d_dig.cpu().numpy()
         bad = np.nonzero((got != want).any(axis=1))[0]
-        assert bad.size == 0, f"unit {unit} aligned={aligned}: {bad.size} bad, first {bad[:8]}"
+        assert bad.size == 0, f"unit {unit} n={n} aligned={aligned}: {bad.size} bad, first {bad[:8]}"
