@@ -117,6 +117,7 @@ def main():
                "py_runs_s": [round(t, 4) for t in py_t],
                "stream_slots": os.environ.get("SHA1CHUNK_STREAM_SLOTS", "default"),
                "stream_slot_mib": os.environ.get("SHA1CHUNK_STREAM_SLOT_MIB", "default"),
+               "read_threads": os.environ.get("SHA1CHUNK_READ_THREADS", "default"),
                "page_cache_read_GiBps": round(read_gibs, 3),
                "pinned_h2d_GiBps": round(h2d, 3), "digests_spot_checked_ok": bool(ok)}
         print(json.dumps(row), flush=True)
