@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
 #include <mutex>
 #include <numeric>
 #include <string>
@@ -29,6 +30,108 @@
 #include "sha1_kernels.h"
 
 namespace {
+// Persistent helper threads that run the parts of one job (a host copy
+// split in pieces, a file read split over pread calls) together with the
+// calling thread.  run() returns when every part is done.  Between jobs the
+// helpers poll for the next one for a while (a caller streaming chunks or
+// file pieces comes back within microseconds) before sleeping, so a job does
+// not pay a thread start or a futex wake-up.
+class PartPool {
+public:
+    explicit PartPool(int helpers) {
+        for (int i = 0; i < helpers; ++i) th_.emplace_back([this] { loop(); });
+    }
+    ~PartPool() {
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            stop_.store(true);
+        }
+        cv_.notify_all();
+        for (auto& t : th_) t.join();
+    }
+    size_t width() const { return th_.size() + 1; }
+    // fn(i) for i in [0, parts), on the caller and the helpers
+    void run(size_t parts, const std::function<void(size_t)>& fn) {
+        if (parts <= 1 || th_.empty()) {
+            for (size_t i = 0; i < parts; ++i) fn(i);
+            return;
+        }
+        {
+            std::lock_guard<std::mutex> g(mu_);
+            fn_ = &fn;
+            parts_.store(parts);
+            left_.store(parts);
+            next_.store(0);
+            gen_.fetch_add(1);
+        }
+        // helpers still polling see gen_ at once; only sleeping ones need the
+        // (syscall) wake-up
+        if (sleepers_.load() > 0) cv_.notify_all();
+        work();
+        // the caller's own parts are done; wait for the helpers' parts
+        for (int spin = 0; left_.load() != 0 && spin < 200000; ++spin) __builtin_ia32_pause();
+        if (left_.load() != 0) {
+            std::unique_lock<std::mutex> g(mu_);
+            done_.wait(g, [this] { return left_.load() == 0; });
+        }
+    }
+
+private:
+    static constexpr int kSpin = 20000;  // pause loops (tens of microseconds)
+    void work() {
+        for (size_t i; (i = next_.fetch_add(1)) < parts_.load();) {
+            (*fn_)(i);
+            if (left_.fetch_sub(1) == 1) {
+                std::lock_guard<std::mutex> g(mu_);
+                done_.notify_all();
+            }
+        }
+    }
+    void loop() {
+        uint64_t seen = 0;
+        for (;;) {
+            int spin = 0;
+            while (gen_.load() == seen && !stop_.load() && spin++ < kSpin) __builtin_ia32_pause();
+            if (gen_.load() == seen && !stop_.load()) {
+                std::unique_lock<std::mutex> g(mu_);
+                sleepers_.fetch_add(1);
+                cv_.wait(g, [&] { return stop_.load() || gen_.load() != seen; });
+                sleepers_.fetch_sub(1);
+            }
+            if (stop_.load()) return;
+            {
+                // a job's fields are published under mu_
+                std::lock_guard<std::mutex> g(mu_);
+                seen = gen_.load();
+            }
+            work();
+        }
+    }
+    std::vector<std::thread> th_;
+    std::mutex mu_;
+    std::condition_variable cv_, done_;
+    std::atomic<uint64_t> gen_{0};
+    std::atomic<int> sleepers_{0};
+    std::atomic<bool> stop_{false};
+    const std::function<void(size_t)>* fn_ = nullptr;
+    std::atomic<size_t> parts_{0};
+    std::atomic<size_t> next_{0};
+    std::atomic<size_t> left_{0};
+};
+
+// memcpy split over a pool (pieces of >= 64 KiB)
+void pool_copy(PartPool& pool, uint8_t* dst, const uint8_t* src, size_t n) {
+    const size_t parts = std::min<size_t>(pool.width(), n / (size_t(64) << 10));
+    if (parts <= 1) {
+        memcpy(dst, src, n);
+        return;
+    }
+    pool.run(parts, [&](size_t i) {
+        const size_t a = n * i / parts, b = n * (i + 1) / parts;
+        memcpy(dst + a, src + a, b - a);
+    });
+}
+
 
 thread_local std::string t_err;
 thread_local int t_dev = 0;
@@ -75,6 +178,15 @@ size_t stream_slot_bytes() {
         const char* e = getenv("SHA1CHUNK_STREAM_SLOT_MIB");
         const size_t mib = e ? std::min<size_t>(1024, std::max<size_t>(16, atoi(e))) : 512;
         return mib << 20;  // a multiple of SHA1CHUNK_CHUNK_LEN
+    }();
+    return b;
+}
+
+// H2D piece of the stream pipeline (SHA1CHUNK_STREAM_PIECE_MIB, 0 = whole slot)
+size_t stream_piece_bytes() {
+    static const size_t b = [] {
+        const char* e = getenv("SHA1CHUNK_STREAM_PIECE_MIB");
+        return static_cast<size_t>(e ? std::max(0, atoi(e)) : 64) << 20;
     }();
     return b;
 }
@@ -664,17 +776,27 @@ long hash_stream_sized(sha1chunk_reader_fn reader, void* reader_ctx, sha1chunk_s
             (rc = s.hdig.ensure(per_slot * 20)) || (rc = s.ddig.ensure(per_slot * 20)))
             return rc;
         uint8_t* h = static_cast<uint8_t*>(s.hpin.p);
+        uint8_t* d = static_cast<uint8_t*>(s.dmem.p);
         // Read straight into pinned memory: the fread loop of make_chunks
-        // (chunk.c:22), a slot of 512 chunks at a time.
-        size_t got = 0;
+        // (chunk.c:22), a slot of up to 1024 chunks at a time, read in pieces
+        // whose H2D copies start as soon as each piece is in, so the copy
+        // engine is not idle while a whole slot is read (the first slot
+        // above all); the kernel still waits for the whole slot.
+        const size_t piece = stream_piece_bytes() ? stream_piece_bytes() : slot_bytes;
+        size_t got = 0, sent = 0;
         while (got < slot_bytes) {
-            const size_t r = reader(reader_ctx, h + meta + got, slot_bytes - got);
+            const size_t r = reader(reader_ctx, h + meta + got, std::min(piece, slot_bytes - got));
             if (r == (size_t)-1) return fail(SHA1CHUNK_EIO, "stream read error");
             if (r == 0) {
                 eof = true;
                 break;
             }
             got += r;
+            if (got - sent >= piece && got < slot_bytes) {
+                HIP_TRY(hipMemcpyAsync(d + meta + sent, h + meta + sent, got - sent, hipMemcpyHostToDevice,
+                                       D->copy));
+                sent = got;
+            }
         }
         if (got == 0) break;
         const size_t m = (got + SHA1CHUNK_CHUNK_LEN - 1) / SHA1CHUNK_CHUNK_LEN;
@@ -685,9 +807,9 @@ long hash_stream_sized(sha1chunk_reader_fn reader, void* reader_ctx, sha1chunk_s
             hlen[j] = static_cast<uint32_t>(
                 std::min<size_t>(SHA1CHUNK_CHUNK_LEN, got - j * SHA1CHUNK_CHUNK_LEN));
         }
-        HIP_TRY(hipMemcpyAsync(s.dmem.p, h, meta + got, hipMemcpyHostToDevice, D->copy));
+        HIP_TRY(hipMemcpyAsync(d + meta + sent, h + meta + sent, got - sent, hipMemcpyHostToDevice, D->copy));
+        HIP_TRY(hipMemcpyAsync(d, h, m * 12, hipMemcpyHostToDevice, D->copy));  // offsets + lengths
         if ((rc = copies_issued(*D, s))) return rc;
-        uint8_t* d = static_cast<uint8_t*>(s.dmem.p);
         BatchArgs A{};
         A.base = d;
         A.off = reinterpret_cast<const uint64_t*>(d);
@@ -743,14 +865,14 @@ static size_t fd_reader(void* ctx, void* dst, size_t n) {
 struct ParFile {
     int fd;
     off_t pos, end;
-    int threads;
+    PartPool* pool;
 };
 static size_t par_reader(void* ctx, void* dst, size_t n) {
     ParFile* f = static_cast<ParFile*>(ctx);
     if (f->pos >= f->end) return 0;
     const size_t want = std::min<size_t>(n, static_cast<size_t>(f->end - f->pos));
     const size_t min_piece = size_t(8) << 20;
-    const int T = static_cast<int>(std::max<size_t>(1, std::min<size_t>(f->threads, want / min_piece)));
+    const int T = static_cast<int>(std::max<size_t>(1, std::min<size_t>(f->pool->width(), want / min_piece)));
     const size_t piece = (want + T - 1) / T;
     std::vector<size_t> got(T, 0);
     std::atomic<bool> bad{false};
@@ -768,10 +890,7 @@ static size_t par_reader(void* ctx, void* dst, size_t n) {
             got[t] += static_cast<size_t>(r);
         }
     };
-    std::vector<std::thread> th;
-    for (int t = 1; t < T; ++t) th.emplace_back(work, t);
-    work(0);
-    for (auto& x : th) x.join();
+    f->pool->run(static_cast<size_t>(T), [&](size_t t) { work(static_cast<int>(t)); });
     if (bad) return (size_t)-1;
     // bytes read contiguously from pos (a short piece ends the file)
     size_t total = 0;
@@ -800,7 +919,8 @@ long sha1chunk_hash_fd(int fd, uint8_t* digests, size_t max_chunks, size_t* tota
     long n;
     if (fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && pos >= 0) {
         const char* e = getenv("SHA1CHUNK_READ_THREADS");
-        ParFile f{fd, pos, std::max(pos, st.st_size), e ? std::max(1, atoi(e)) : 8};
+        PartPool pool((e ? std::max(1, atoi(e)) : 8) - 1);
+        ParFile f{fd, pos, std::max(pos, st.st_size), &pool};
         n = hash_stream_sized(par_reader, &f, fd_sink, &sk, static_cast<uint64_t>(f.end - f.pos));
         (void)lseek(fd, f.pos, SEEK_SET);
     } else {
@@ -909,101 +1029,6 @@ int sha1chunk_synth_fill_ragged_async(void* d_base, const uint64_t* d_offsets,
 namespace {
 constexpr int kVqSets = 3;
 
-// Helper threads that split one large host copy (a submitted 512 KiB chunk
-// into pinned staging) so that the copy, not one core's memcpy rate
-// (~10-20 GB/s), bounds the queue.  copy() returns when every byte is
-// written, so the caller may reuse its buffer as with one memcpy.
-class CopyPool {
-public:
-    explicit CopyPool(int helpers) {
-        for (int i = 0; i < helpers; ++i) th_.emplace_back([this] { run(); });
-    }
-    ~CopyPool() {
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            stop_.store(true);
-        }
-        cv_.notify_all();
-        for (auto& t : th_) t.join();
-    }
-    void copy(uint8_t* dst, const uint8_t* src, size_t n) {
-        const size_t parts = std::min<size_t>(th_.size() + 1, n / kMinPiece);
-        if (parts <= 1) {
-            memcpy(dst, src, n);
-            return;
-        }
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            dst_ = dst;
-            src_ = src;
-            n_ = n;
-            parts_.store(parts);
-            left_.store(static_cast<int>(parts));
-            next_.store(0);
-            gen_.fetch_add(1);
-        }
-        // helpers still spinning from the previous copy see gen_ at once;
-        // only sleeping ones need the (syscall) wake-up
-        if (sleepers_.load() > 0) cv_.notify_all();
-        work();
-        // the caller's own pieces are done; wait for the helpers' pieces
-        for (int spin = 0; left_.load() != 0 && spin < 200000; ++spin) __builtin_ia32_pause();
-        if (left_.load() != 0) {
-            std::unique_lock<std::mutex> g(mu_);
-            done_.wait(g, [this] { return left_.load() == 0; });
-        }
-    }
-
-private:
-    static constexpr size_t kMinPiece = size_t(64) << 10;
-    // A helper keeps polling for the next copy this many pause loops (tens of
-    // microseconds: a submitter streaming chunks comes back sooner) before it
-    // sleeps on the condition variable.
-    static constexpr int kSpin = 20000;
-    void work() {
-        for (size_t i; (i = next_.fetch_add(1)) < parts_.load();) {
-            const size_t P = parts_.load(), a = n_ * i / P, b = n_ * (i + 1) / P;
-            memcpy(dst_ + a, src_ + a, b - a);
-            if (left_.fetch_sub(1) == 1) {
-                std::lock_guard<std::mutex> g(mu_);
-                done_.notify_all();
-            }
-        }
-    }
-    void run() {
-        uint64_t seen = 0;
-        for (;;) {
-            int spin = 0;
-            while (gen_.load() == seen && !stop_.load() && spin++ < kSpin) __builtin_ia32_pause();
-            if (gen_.load() == seen && !stop_.load()) {
-                std::unique_lock<std::mutex> g(mu_);
-                sleepers_.fetch_add(1);
-                cv_.wait(g, [&] { return stop_.load() || gen_.load() != seen; });
-                sleepers_.fetch_sub(1);
-            }
-            if (stop_.load()) return;
-            {
-                // fields of generation gen_ are published under mu_
-                std::lock_guard<std::mutex> g(mu_);
-                seen = gen_.load();
-            }
-            work();
-        }
-    }
-    std::vector<std::thread> th_;
-    std::mutex mu_;
-    std::condition_variable cv_, done_;
-    std::atomic<uint64_t> gen_{0};
-    std::atomic<int> sleepers_{0};
-    std::atomic<bool> stop_{false};
-    uint8_t* dst_ = nullptr;
-    const uint8_t* src_ = nullptr;
-    size_t n_ = 0;
-    std::atomic<size_t> parts_{0};
-    std::atomic<size_t> next_{0};
-    std::atomic<int> left_{0};
-};
-
 int vq_copy_helpers() {
     const char* e = getenv("SHA1CHUNK_VQ_THREADS");
     // threads in all, the caller included; 4 measured best on the GPU box
@@ -1034,7 +1059,7 @@ struct sha1chunk_vq {
     std::deque<int> flight;  // launched sets, oldest first
     std::deque<std::pair<uint64_t, uint8_t>> ready;
     size_t pending = 0;
-    CopyPool* copier = nullptr;
+    PartPool* copier = nullptr;
 };
 
 namespace {
@@ -1104,7 +1129,7 @@ sha1chunk_vq* sha1chunk_vq_create(size_t batch, uint32_t max_chunk_len) {
     q->maxlen = max_chunk_len;
     q->stride = round_up(max_chunk_len, kAlign);
     q->meta = round_up(batch * (8 + 4 + 20), kAlign);
-    q->copier = new CopyPool(vq_copy_helpers());
+    q->copier = new PartPool(vq_copy_helpers());
     const size_t hbytes = q->meta + batch * q->stride;
     for (auto& S : q->set) {
         if (S.h.ensure(hbytes) || S.d.ensure(hbytes + batch * 21) || S.res.ensure(batch) ||
@@ -1133,7 +1158,7 @@ int sha1chunk_vq_submit(sha1chunk_vq* q, const void* chunk, uint32_t len, const 
     vq_off(q, h)[i] = q->meta + i * q->stride;
     vq_len(q, h)[i] = len;
     memcpy(vq_exp(q, h) + 20 * i, expected, 20);
-    if (len) q->copier->copy(h + q->meta + i * q->stride, static_cast<const uint8_t*>(chunk), len);
+    if (len) pool_copy(*q->copier, h + q->meta + i * q->stride, static_cast<const uint8_t*>(chunk), len);
     S->tags.push_back(tag);
     ++S->count;
     ++q->pending;

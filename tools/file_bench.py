@@ -118,6 +118,7 @@ def main():
                "stream_slots": os.environ.get("SHA1CHUNK_STREAM_SLOTS", "default"),
                "stream_slot_mib": os.environ.get("SHA1CHUNK_STREAM_SLOT_MIB", "default"),
                "read_threads": os.environ.get("SHA1CHUNK_READ_THREADS", "default"),
+               "stream_piece_mib": os.environ.get("SHA1CHUNK_STREAM_PIECE_MIB", "default"),
                "page_cache_read_GiBps": round(read_gibs, 3),
                "pinned_h2d_GiBps": round(h2d, 3), "digests_spot_checked_ok": bool(ok)}
         print(json.dumps(row), flush=True)
