@@ -18,6 +18,7 @@
 #include <cstring>
 #include <deque>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <numeric>
 #include <string>
@@ -255,6 +256,9 @@ struct Device {
     hipStream_t copy = nullptr;
     DevBuf small;  // streaming calls: state + data
     PinBuf small_pin;
+    // threads that pack pageable host chunks into pinned staging (created on
+    // the first such batch, alive with the process; idle ones sleep)
+    std::unique_ptr<PartPool> pack;
 };
 
 std::once_flag g_once;
@@ -413,37 +417,29 @@ bool host_pinned(const void* p) {
     return at.type == hipMemoryTypeHost;
 }
 
-// Pack a slot's chunks from pageable caller memory into pinned staging with
-// several threads: one thread copies ~10 GB/s, well under the PCIe rate.
-void pack_parallel(uint8_t* h, const uint64_t* hoff, const uint8_t* base, const uint64_t* offsets,
-                   const uint32_t* lengths, const std::vector<uint32_t>& ids, size_t bytes) {
-    static const int kThreads = [] {
-        const char* e = getenv("SHA1CHUNK_COPY_THREADS");
-        return e ? std::max(1, atoi(e)) : 8;
-    }();
-    const size_t m = ids.size();
-    const int T = static_cast<int>(std::min<size_t>(kThreads, std::max<size_t>(1, bytes >> 24)));
-    auto work = [&](size_t j0, size_t j1) {
-        for (size_t j = j0; j < j1; ++j)
+// Pack entries [j0, j1) of a slot from pageable caller memory into pinned
+// staging on the device's pack pool: one thread copies ~10 GB/s, well under
+// the PCIe rate.  The entries are split into pool-width runs of about equal
+// bytes.
+int pack_threads() {
+    const char* e = getenv("SHA1CHUNK_COPY_THREADS");
+    return e ? std::max(1, atoi(e)) : 8;
+}
+void pack_range(PartPool& pool, uint8_t* h, const uint64_t* hoff, const uint8_t* base,
+                const uint64_t* offsets, const uint32_t* lengths, const std::vector<uint32_t>& ids,
+                size_t j0, size_t j1, size_t bytes) {
+    const size_t T = std::min<size_t>(pool.width(), std::max<size_t>(1, bytes >> 23));
+    std::vector<size_t> cut(T + 1, j1);
+    cut[0] = j0;
+    for (size_t t = 1, j = j0; t < T; ++t) {
+        const uint64_t target = hoff[j0] + bytes * t / T;
+        while (j < j1 && hoff[j] < target) ++j;
+        cut[t] = j;
+    }
+    pool.run(T, [&](size_t t) {
+        for (size_t j = cut[t]; j < cut[t + 1]; ++j)
             if (lengths[ids[j]]) memcpy(h + hoff[j], base + offsets[ids[j]], lengths[ids[j]]);
-    };
-    if (T == 1) {
-        work(0, m);
-        return;
-    }
-    // contiguous entry ranges of about bytes/T each
-    std::vector<std::thread> th;
-    size_t j0 = 0;
-    const uint64_t start = hoff[0];
-    for (int t = 1; t < T && j0 < m; ++t) {
-        const uint64_t target = start + bytes * t / T;
-        size_t j1 = j0;
-        while (j1 < m && hoff[j1] < target) ++j1;
-        if (j1 > j0) th.emplace_back(work, j0, j1);
-        j0 = j1;
-    }
-    work(j0, m);
-    for (auto& x : th) x.join();
+    });
 }
 
 int stage_and_launch(Device& D, Slot& s, const uint8_t* base, const uint64_t* offsets,
@@ -481,13 +477,28 @@ int stage_and_launch(Device& D, Slot& s, const uint8_t* base, const uint64_t* of
             cur += round_up(L, kAlign);
         }
     }
-    if (!direct) pack_parallel(h, hoff, base, offsets, lengths, s.ids, cur - meta);
     uint8_t* d = static_cast<uint8_t*>(s.dmem.p);
     if (direct) {
         HIP_TRY(hipMemcpyAsync(d, h, meta, hipMemcpyHostToDevice, D.copy));
         if (span) HIP_TRY(hipMemcpyAsync(d + meta, base + span0, span, hipMemcpyHostToDevice, D.copy));
     } else {
-        HIP_TRY(hipMemcpyAsync(d, h, cur, hipMemcpyHostToDevice, D.copy));
+        // pack in runs of ~64 MiB and start each run's H2D as soon as it is
+        // packed, so the copy engine works while the rest is packed
+        if (!D.pack) D.pack.reset(new PartPool(pack_threads() - 1));
+        static const size_t piece = [] {  // SHA1CHUNK_PACK_PIECE_MIB, 0 = whole slot
+            const char* e = getenv("SHA1CHUNK_PACK_PIECE_MIB");
+            const size_t mib = e ? static_cast<size_t>(std::max(0, atoi(e))) : 64;
+            return mib ? mib << 20 : ~size_t(0) >> 1;
+        }();
+        for (size_t j0 = 0; j0 < m;) {
+            size_t j1 = j0 + 1;
+            while (j1 < m && hoff[j1] - hoff[j0] < piece) ++j1;
+            const size_t end = j1 < m ? hoff[j1] : cur;
+            pack_range(*D.pack, h, hoff, base, offsets, lengths, s.ids, j0, j1, end - hoff[j0]);
+            HIP_TRY(hipMemcpyAsync(d + hoff[j0], h + hoff[j0], end - hoff[j0], hipMemcpyHostToDevice, D.copy));
+            j0 = j1;
+        }
+        HIP_TRY(hipMemcpyAsync(d, h, meta, hipMemcpyHostToDevice, D.copy));
     }
     if ((rc = copies_issued(D, s))) return rc;
     BatchArgs A{};
