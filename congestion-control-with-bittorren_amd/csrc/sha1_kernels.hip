@@ -14,7 +14,7 @@
 //   sha1_fused_kernel  one wave per 64 chunks, schedule + rounds in VGPRs
 //                      (~627 instructions per block), two 128-byte stages of
 //                      each chunk prefetched per lane.  The high-occupancy
-//                      kernel: >= 2 groups of 64 chunks per CU.
+//                      kernel: > 2 groups of 64 chunks per CU.
 //   sha1_split_kernel  workgroup = consumer wave + producer wave(s) on the
 //                      same 64 chunks.  Producers stream and byte-swap the
 //                      blocks and expand the 80-word schedule (+K) into an
@@ -22,6 +22,13 @@
 //                      instructions per block instead of ~627), which is the
 //                      bound when there are too few chunks to fill the
 //                      SIMDs (BASELINE config 2: 4096 chunks = 64 waves).
+//                      One wave's 20 ds_write_b128 per block cost ~28 cycles
+//                      each on top of its VALU (tools/gen_producer_probe.py),
+//                      so one producer is as slow as the consumer: each
+//                      consumer gets two producers, laid out so that it has a
+//                      SIMD to itself (a workgroup's waves 0-3 land on four
+//                      different SIMDs, wave w + 4 on wave w's:
+//                      tools/wave_placement_probe.hip).
 //
 // Measured on MI355X (tools/issue_probe.hip, tools/gen_consumer_probe.py,
 // DESIGN.md section 5): one wave issues at most one instruction per 4.0
