@@ -1,0 +1,71 @@
+"""Seeded randomized parity: many small ragged batches through every kernel
+and every split shape the library builds, bit-exact against the oracle
+(oracle/sha1_oracle.c, pinned to the reference's golden vectors by
+tests/test_oracle.py).  Lengths concentrate on the padding boundaries of
+sha.c:536-543 (len % 64 in {55, 56, 63, 0}) and the 16-byte alignment the
+bulk load paths depend on."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+KERNELS = ["lane", "fused", "split", "auto"]
+SPLIT_UNITS = [1, 2, 3, 4, 8, 9, 10, 11, 12, 505, 569, 577]
+
+
+def _lengths(rng, n):
+    kind = rng.integers(0, 4, n)
+    base = rng.integers(0, 3000, n) * 64
+    edge = rng.choice(np.array([0, 1, 55, 56, 57, 63, 64, 65, 119, 120, 127, 128]), n)
+    lens = np.where(kind == 0, base + edge,                       # near block edges
+           np.where(kind == 1, rng.integers(0, 200000, n),        # anything
+           np.where(kind == 2, 65536 + rng.integers(-70, 70, n),  # long, near-equal
+                    edge)))                                        # tiny
+    return np.clip(lens, 0, None).astype(np.uint32)
+
+
+@pytest.fixture(scope="module")
+def dev(pkg):
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a device"
+    torch.cuda.set_device(0)
+    pkg.set_device(0)
+    return torch
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_batches_every_kernel(pkg, dev, oracle, seed, monkeypatch):
+    torch = dev
+    rng = np.random.default_rng(7000 + seed)
+    n = int(rng.integers(1, 400))
+    lens = _lengths(rng, n)
+    align = int(rng.choice([1, 4, 16, 64]))
+    step = (lens.astype(np.uint64) + np.uint64(align - 1)) // np.uint64(align) * np.uint64(align)
+    step += rng.integers(0, 3, n).astype(np.uint64) * np.uint64(align)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(step)[: n - 1]
+    off += np.uint64(int(rng.integers(0, 4)) * align)
+    host = rng.integers(0, 256, int(off[-1] + lens[-1]) + 64, dtype=np.uint8)
+    want = oracle.hash_batch(host, off, lens)
+    d_host = torch.from_numpy(host).cuda()
+    d_off = torch.from_numpy(off.astype(np.int64)).cuda()
+    d_len = torch.from_numpy(lens.astype(np.int32)).cuda()
+    kernels = KERNELS + [f"split:{u}" for u in rng.choice(SPLIT_UNITS, 3, replace=False)]
+    for k in kernels:
+        if k.startswith("split:"):
+            monkeypatch.setenv("SHA1CHUNK_SPLIT_UNIT", k.split(":")[1])
+            name = "split"
+        else:
+            monkeypatch.delenv("SHA1CHUNK_SPLIT_UNIT", raising=False)
+            name = k
+        dig = torch.zeros((n, 20), dtype=torch.uint8, device="cuda")
+        pkg.hash_device(d_host, d_off, d_len, dig, kernel=name)
+        torch.cuda.synchronize()
+        got = dig.cpu().numpy()
+        bad = np.nonzero((got != want).any(axis=1))[0]
+        assert bad.size == 0, f"seed {seed} kernel {k} n={n} align={align}: {bad.size} bad, " \
+                              f"first {bad[:6]} lens {lens[bad[:6]]}"
+    monkeypatch.delenv("SHA1CHUNK_SPLIT_UNIT", raising=False)
+    # the host-memory path (pageable numpy): packing + pipeline
+    got = pkg.hash_batch(host, off, lens)
+    assert np.array_equal(got, want), f"seed {seed}: host batch"
