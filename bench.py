@@ -26,6 +26,7 @@ from __future__ import annotations
 
 import argparse
 import glob
+import hashlib
 import importlib
 import json
 import os
@@ -38,6 +39,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "GiB/s device-resident SHA-1 over 512KB chunks; % of HBM-read roofline"
+CHUNK_LEN = 524288  # constants.h:14
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 # Per-chunk serial floor: a rounds-only wave needs 5 VALU per round x 80
 # rounds per 64-B block, and one wave issues one instruction per 4.0 cycles
@@ -135,20 +137,22 @@ def main():
     elapsed, kern_ms = shard.max_over_ranks([t1 - t0, kern_ms], device=cdev)
 
     # ---- parity of the timed output (every rank, against the reference) ----
-    from oracle import oracle as O  # checker only
+    # Checked with the standard library's SHA-1 (hashlib), independent of
+    # both the engine and oracle/: the digest-of-digests of a 4096-chunk
+    # range against the reference-generated golden aggregate, otherwise a
+    # sample of chunks re-hashed from the device buffer's own bytes.
     golden = json.load(open(os.path.join(ROOT, "tests/golden/golden.json")))
     parity = True
     for p in range(P):
         got = digs[p].cpu().numpy()
         b = first // n + p  # index of this batch's 4096-chunk range
-        if n == 4096 and L == O.CHUNK_LEN and b < len(golden["weak4096"]):
-            parity &= O.digest_of_digests(got).hex() == golden["weak4096"][b]
+        if n == 4096 and L == CHUNK_LEN and b < len(golden["weak4096"]):
+            parity &= hashlib.sha1(got.tobytes()).hexdigest() == golden["weak4096"][b]
         else:
             idx = np.unique(np.linspace(0, n - 1, min(n, 16)).astype(np.int64))
-            host = np.concatenate([O.synth_chunks(first + p * n + int(i), 1, L) for i in idx])
-            want = O.hash_batch(host, np.arange(idx.size, dtype=np.uint64) * L,
-                                np.full(idx.size, L, np.uint32))
-            parity &= bool(np.array_equal(got[idx], want))
+            for i in idx:
+                chunk = bufs[p][int(i) * L:(int(i) + 1) * L].cpu().numpy().tobytes()
+                parity &= hashlib.sha1(chunk).digest() == got[int(i)].tobytes()
     parity = shard.all_ranks_ok(parity, device=cdev)
 
     ms_per_step = elapsed / a.steps * 1e3
@@ -203,6 +207,7 @@ def main():
         },
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        from oracle import oracle as O  # the CPU baseline leg only: the reference sha.c, timed
         result["cpu_baseline"] = _cpu_baseline(O, n, L, a.cpu_threads, golden)
     if rank == 0:
         print(json.dumps(result), flush=True)
