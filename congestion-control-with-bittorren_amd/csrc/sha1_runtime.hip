@@ -1062,7 +1062,8 @@ struct VqSet {
 struct sha1chunk_vq {
     int dev = 0;
     int cus = 256;
-    size_t batch = 0;
+    size_t batch = 0;  // launch threshold
+    size_t cap = 0;    // chunks a set holds: a batch grows up to this while the device is busy
     uint32_t maxlen = 0;
     size_t stride = 0, meta = 0;
     VqSet set[kVqSets];
@@ -1077,9 +1078,9 @@ namespace {
 
 uint64_t* vq_off(sha1chunk_vq* q, uint8_t* base) { return reinterpret_cast<uint64_t*>(base); }
 uint32_t* vq_len(sha1chunk_vq* q, uint8_t* base) {
-    return reinterpret_cast<uint32_t*>(base + q->batch * 8);
+    return reinterpret_cast<uint32_t*>(base + q->cap * 8);
 }
-uint8_t* vq_exp(sha1chunk_vq* q, uint8_t* base) { return base + q->batch * 12; }
+uint8_t* vq_exp(sha1chunk_vq* q, uint8_t* base) { return base + q->cap * 12; }
 
 int vq_launch(sha1chunk_vq* q, int which) {
     VqSet& S = q->set[which];
@@ -1088,8 +1089,8 @@ int vq_launch(sha1chunk_vq* q, int which) {
     uint8_t* h = static_cast<uint8_t*>(S.h.p);
     uint8_t* d = static_cast<uint8_t*>(S.d.p);
     HIP_TRY(hipMemcpyAsync(d, h, q->meta + S.count * q->stride, hipMemcpyHostToDevice, S.stream));
-    uint8_t* ddig = d + q->meta + q->batch * q->stride;
-    uint8_t* dmis = ddig + q->batch * 20;
+    uint8_t* ddig = d + q->meta + q->cap * q->stride;
+    uint8_t* dmis = ddig + q->cap * 20;
     BatchArgs A{};
     A.base = d;
     A.off = vq_off(q, d);
@@ -1122,6 +1123,44 @@ int vq_collect_oldest(sha1chunk_vq* q) {
     return SHA1CHUNK_OK;
 }
 
+// Collect every launched set that has finished, oldest first, without
+// blocking.
+int vq_reap(sha1chunk_vq* q) {
+    while (!q->flight.empty()) {
+        hipError_t e = hipEventQuery(q->set[q->flight.front()].done);
+        if (e == hipErrorNotReady) break;
+        if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "vq: %s", hipGetErrorString(e));
+        int rc = vq_collect_oldest(q);
+        if (rc) return rc;
+    }
+    return SHA1CHUNK_OK;
+}
+
+// Launch the fill set once it holds `batch` chunks, unless the device is
+// busy with kVqSets - 1 earlier sets: then the set keeps growing, a batch at
+// a time (up to `cap`), and goes at the first whole batch after one of them
+// finishes.  Every launch costs at
+// least one chunk's serial hash time (~6 ms), so while the device is busy a
+// bigger batch is free throughput; while it is idle, `batch` bounds latency.
+int vq_maybe_launch(sha1chunk_vq* q) {
+    VqSet& S = q->set[q->fill];
+    // only at whole multiples of `batch`: a caller that submits whole batches
+    // still gets every result back through non-blocking polls, no flush
+    if (S.inflight || S.count < q->batch || S.count % q->batch) return SHA1CHUNK_OK;
+    int rc = vq_reap(q);
+    if (rc) return rc;
+    if (S.count < q->cap && q->flight.size() >= static_cast<size_t>(kVqSets - 1)) return SHA1CHUNK_OK;
+    if ((rc = vq_launch(q, q->fill))) return rc;
+    q->fill = (q->fill + 1) % kVqSets;
+    return SHA1CHUNK_OK;
+}
+
+size_t vq_cap(size_t batch) {
+    const char* e = getenv("SHA1CHUNK_VQ_GROW");  // 0: launch at exactly `batch`
+    if ((e && atoi(e) == 0) || batch >= 512) return batch;
+    return std::max(batch, std::min(4 * batch, 512 / batch * batch));  // a multiple of batch
+}
+
 }  // namespace
 
 extern "C" {
@@ -1137,20 +1176,21 @@ sha1chunk_vq* sha1chunk_vq_create(size_t batch, uint32_t max_chunk_len) {
     q->dev = D->id;
     q->cus = D->cus;
     q->batch = batch;
+    q->cap = vq_cap(batch);
     q->maxlen = max_chunk_len;
     q->stride = round_up(max_chunk_len, kAlign);
-    q->meta = round_up(batch * (8 + 4 + 20), kAlign);
+    q->meta = round_up(q->cap * (8 + 4 + 20), kAlign);
     q->copier = new PartPool(vq_copy_helpers());
-    const size_t hbytes = q->meta + batch * q->stride;
+    const size_t hbytes = q->meta + q->cap * q->stride;
     for (auto& S : q->set) {
-        if (S.h.ensure(hbytes) || S.d.ensure(hbytes + batch * 21) || S.res.ensure(batch) ||
+        if (S.h.ensure(hbytes) || S.d.ensure(hbytes + q->cap * 21) || S.res.ensure(q->cap) ||
             hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&S.done, hipEventDisableTiming) != hipSuccess) {
             if (t_err.empty()) fail(SHA1CHUNK_ENOMEM, "vq: allocation failed");
             sha1chunk_vq_destroy(q);
             return nullptr;
         }
-        S.tags.reserve(batch);
+        S.tags.reserve(q->cap);
     }
     return q;
 }
@@ -1164,6 +1204,14 @@ int sha1chunk_vq_submit(sha1chunk_vq* q, const void* chunk, uint32_t len, const 
         int rc = vq_collect_oldest(q);
         if (rc) return rc;
     }
+    if (S->count >= q->cap) {  // only after a failed launch
+        int rc = vq_maybe_launch(q);
+        if (rc) return rc;
+        S = &q->set[q->fill];
+        while (S->inflight) {
+            if ((rc = vq_collect_oldest(q))) return rc;
+        }
+    }
     uint8_t* h = static_cast<uint8_t*>(S->h.p);
     const size_t i = S->count;
     vq_off(q, h)[i] = q->meta + i * q->stride;
@@ -1173,12 +1221,7 @@ int sha1chunk_vq_submit(sha1chunk_vq* q, const void* chunk, uint32_t len, const 
     S->tags.push_back(tag);
     ++S->count;
     ++q->pending;
-    if (S->count == q->batch) {
-        int rc = vq_launch(q, q->fill);
-        if (rc) return rc;
-        q->fill = (q->fill + 1) % kVqSets;
-    }
-    return SHA1CHUNK_OK;
+    return vq_maybe_launch(q);
 }
 
 int sha1chunk_vq_flush(sha1chunk_vq* q) {
@@ -1198,12 +1241,8 @@ long sha1chunk_vq_poll(sha1chunk_vq* q, uint64_t* tags, uint8_t* mismatch, size_
         while (!q->flight.empty())
             if ((rc = vq_collect_oldest(q))) return rc;
     } else {
-        while (!q->flight.empty()) {
-            hipError_t e = hipEventQuery(q->set[q->flight.front()].done);
-            if (e == hipErrorNotReady) break;
-            if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "vq: %s", hipGetErrorString(e));
-            if ((rc = vq_collect_oldest(q))) return rc;
-        }
+        if ((rc = vq_reap(q))) return rc;
+        if ((rc = vq_maybe_launch(q))) return rc;  // a grown batch waiting for the device
     }
     size_t n = 0;
     while (n < max && !q->ready.empty()) {

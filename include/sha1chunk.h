@@ -120,8 +120,13 @@ int sha1chunk_synth_fill_ragged_async(void *d_base, const uint64_t *d_offsets,
  * select() loop (packet_handler.c:469-472 -> job.c:217 verify_hash).  A queue
  * batches them instead: submit() copies the chunk into pinned staging (the
  * caller may reuse its buffer at once) with its expected digest and a tag;
- * every `batch` submissions (or on flush) the batch is hashed and compared on
- * the device asynchronously; poll() returns finished (tag, mismatch) pairs,
+ * once `batch` submissions are pending (or on flush) the batch is hashed and
+ * compared on the device asynchronously -- while two earlier batches are
+ * still on the device a batch keeps growing by whole batches (up to 4 x
+ * batch, at most 512; SHA1CHUNK_VQ_GROW=0 disables) and goes at the first
+ * whole batch after one finishes (a submit or a poll notices); whole batches
+ * therefore always come back through poll() without a flush; poll() returns
+ * finished (tag, mismatch) pairs,
  * mismatch following verify_hash: 0 = match, 1 = mismatch -> re-GET.  One
  * queue per thread; queues on one device share nothing.  The copy is split
  * over SHA1CHUNK_VQ_THREADS threads (default 4, the caller included: three

@@ -420,6 +420,36 @@ def test_verify_queue_receive_path(pkg, dev, oracle, golden, fixture_files):
     assert got == want
 
 
+@pytest.mark.parametrize("grow", ["1", "0"])
+def test_verify_queue_full_batches_drain_by_polling(pkg, dev, monkeypatch, grow):
+    """Submissions in whole batches come back through non-blocking poll()
+    alone (no flush, no wait): a batch held back to grow while two earlier
+    ones are on the device is launched by a later poll once one finishes."""
+    import hashlib
+    import time
+    monkeypatch.setenv("SHA1CHUNK_VQ_GROW", grow)
+    rng = np.random.default_rng(5)
+    bufs = [rng.integers(0, 256, 4096 + 64 * k, dtype=np.uint8).tobytes() for k in range(16)]
+    batch, n = 8, 8 * 7
+    want, got = {}, {}
+    with pkg.VerifyQueue(batch=batch, max_chunk_len=L512) as q:
+        for t in range(n):
+            b = bufs[t % len(bufs)]
+            d = hashlib.sha1(b).digest()
+            if t % 5 == 3:
+                d = bytes([d[0] ^ 0x80]) + d[1:]
+            want[t] = 1 if t % 5 == 3 else 0
+            q.submit(b, d, t)
+        t0 = time.time()
+        while len(got) < n and time.time() - t0 < 30:
+            for tag, m in q.poll():
+                assert tag not in got
+                got[tag] = m
+            time.sleep(0.001)
+        assert q.pending == 0
+    assert got == want
+
+
 # ------------------------------------- sender verify + master index ----
 _VERIFY_DRIVER = r'''
 #include <stdio.h>
