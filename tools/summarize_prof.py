@@ -10,10 +10,12 @@ import shutil
 import sys
 
 tag, out_tag = sys.argv[1], sys.argv[2]
+n = int(sys.argv[3]) if len(sys.argv) > 3 else 4096  # chunks per launch (bench --chunks)
+name = "bench" if n == 4096 else f"bench_{n}"
 src = f"gpurun_out/prof_{tag}"
 dst = "profiles"
-shutil.copy(f"{src}/trace/run_kernel_stats.csv", f"{dst}/rocprof_bench_{out_tag}_kernel_stats.csv")
-shutil.copy(f"{src}/sq/run_counter_collection.csv", f"{dst}/rocprof_bench_{out_tag}_sq_counters.csv")
+shutil.copy(f"{src}/trace/run_kernel_stats.csv", f"{dst}/rocprof_{name}_{out_tag}_kernel_stats.csv")
+shutil.copy(f"{src}/sq/run_counter_collection.csv", f"{dst}/rocprof_{name}_{out_tag}_sq_counters.csv")
 
 
 def per_kernel(path, counter):
@@ -27,13 +29,14 @@ def per_kernel(path, counter):
 
 k, fetch = per_kernel(f"{src}/fetch/run_counter_collection.csv", "FETCH_SIZE")
 _, write = per_kernel(f"{src}/write/run_counter_collection.csv", "WRITE_SIZE")
-n, L = 4096, 524288
+L = 524288
 f_kb, w_kb = sum(fetch) / len(fetch), sum(write) / len(write)
 rd, wr = 2 * f_kb * 1024, w_kb * 1024
 alg = n * (L + 20)
 rec = {
     "source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, of `python3 bench.py "
-              "--steps 10 --warmup 2 --no-cpu-baseline` (tools/profile_bench.sh)",
+              f"--steps 10 --warmup 2 --no-cpu-baseline{'' if n == 4096 else f' --chunks {n}'}` "
+              "(tools/profile_bench.sh)",
     "kernel": k, "chunks": n, "chunk_bytes": L, "dispatches": len(fetch),
     "fetch_size_kb_per_dispatch": f_kb, "write_size_kb_per_dispatch": w_kb,
     "correction": "gfx950 FETCH_SIZE reports half the bytes of a wide streaming read "
@@ -42,5 +45,6 @@ rec = {
     "read_bytes_per_launch": rd, "write_bytes_per_launch": wr, "bytes_per_launch": rd + wr,
     "algorithmic_bytes_per_launch": alg, "traffic_over_algorithmic": (rd + wr) / alg,
 }
-json.dump(rec, open(f"{dst}/traffic_{out_tag}.json", "w"), indent=1)
+json.dump(rec, open(f"{dst}/traffic_{out_tag}.json" if n == 4096 else f"{dst}/traffic_{n}_{out_tag}.json", "w"),
+          indent=1)
 print(json.dumps(rec, indent=1))
