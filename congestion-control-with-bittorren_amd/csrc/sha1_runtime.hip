@@ -288,9 +288,15 @@ void probe() {
         g_count = 0;
         return;
     }
-    g_count = n;
-    g_dev = new Device[n];
-    for (int d = 0; d < n; ++d) g_dev[d].id = d;
+    // SHA1CHUNK_VIRTUAL_DEVICES=k (testing): k logical devices over the n
+    // physical ones (logical d -> physical d % n), each with its own streams,
+    // slots and host thread, so the multi-device path (SHA1CHUNK_ALL_DEVICES:
+    // byte-balanced slices, one thread per device) runs on a one-GPU box.
+    int k = n;
+    if (const char* e = getenv("SHA1CHUNK_VIRTUAL_DEVICES")) k = std::max(1, std::min(64, atoi(e)));
+    g_count = k;
+    g_dev = new Device[k];
+    for (int d = 0; d < k; ++d) g_dev[d].id = d % n;
 }
 
 int device_count() {

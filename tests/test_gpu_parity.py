@@ -2,6 +2,7 @@
 and the reference's golden vectors.  Bit-exact everywhere (integer work)."""
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -386,6 +387,44 @@ def test_host_batch_all_devices(pkg, dev, oracle, golden):
 
 
 # ------------------------------------------------------- verify queue ----
+_ALL_DEVICES_SCRIPT = r"""
+import hashlib, importlib, sys
+import numpy as np
+sys.path.insert(0, sys.argv[1])
+pkg = importlib.import_module("congestion-control-with-bittorren_amd")
+assert pkg.device_count() == int(sys.argv[2]), pkg.device_count()
+rng = np.random.default_rng(31)
+n = 700
+lens = rng.integers(0, 300000, n).astype(np.uint32)
+lens[:64] = 524288
+lens[100:110] = 0
+off = np.zeros(n, np.uint64)
+off[1:] = np.cumsum(lens.astype(np.uint64) + rng.integers(0, 9, n).astype(np.uint64))[: n - 1]
+buf = rng.integers(0, 256, int(off[-1] + lens[-1]) + 16, dtype=np.uint8)
+want = np.array([np.frombuffer(hashlib.sha1(buf[int(o):int(o) + int(l)].tobytes()).digest(), np.uint8)
+                 for o, l in zip(off, lens)])
+got = pkg.hash_batch(buf, off, lens, all_devices=True)
+assert np.array_equal(got, want), np.nonzero((got != want).any(axis=1))[0][:8]
+assert np.array_equal(pkg.hash_batch(buf, off, lens), want)
+print("all-devices ok")
+"""
+
+
+def test_host_batch_all_devices_virtual(pkg, dev, tmp_path):
+    """SHA1CHUNK_ALL_DEVICES with several devices (byte-balanced
+    slices, one host thread and pipeline per device, no collective), run on
+    a one-GPU box through SHA1CHUNK_VIRTUAL_DEVICES=3 (three logical devices,
+    each with its own streams and slots, over the physical one), in a child
+    process because the device probe happens once per process.  Digests are
+    checked against hashlib."""
+    script = tmp_path / "alldev.py"
+    script.write_text(_ALL_DEVICES_SCRIPT)
+    env = dict(os.environ, SHA1CHUNK_VIRTUAL_DEVICES="3")
+    r = subprocess.run([sys.executable, str(script), ROOT, "3"], capture_output=True, text=True, env=env,
+                       timeout=120)
+    assert r.returncode == 0 and "all-devices ok" in r.stdout, r.stdout + r.stderr
+
+
 def test_verify_queue_receive_path(pkg, dev, oracle, golden, fixture_files):
     """Batched async verify (packet_handler.c:469-472 -> job.c:217): every
     result comes back exactly once with verify_hash's 0/1 convention."""
