@@ -1,0 +1,138 @@
+"""Host C code under AddressSanitizer + UndefinedBehaviorSanitizer (SURVEY.md
+5: the reference builds with -g -Wall only, so the build checks its CPU
+code with sanitizers instead).  CPU only:
+
+* the oracle restatement (oracle/sha1_oracle.c) hashing every length 0..300
+  and a few long ones, one-shot and streamed at odd split points, checked
+  against hashlib;
+* the chunk-file readers of the library (csrc/chunk_file.c, compiled on
+  their own) on CRLF / LF / comment / master-header files, including a digit
+  line without a hash and a hash that is absent.
+Any sanitizer report fails the run (halt_on_error, exit code != 0)."""
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer", "-g", "-O1"]
+ENV = dict(os.environ, ASAN_OPTIONS="halt_on_error=1:detect_leaks=1",
+           UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+
+_ORACLE_DRV = r'''
+#include <stdio.h>
+#include <stdlib.h>
+#include "sha1_oracle.h"
+/* argv[1]: data file; then lengths.  For each length L: one-shot digest of
+ * the first L bytes, and the same L bytes streamed in pieces of 1, 7, 63,
+ * 64, 65, ... bytes; prints "L oneshot streamed". */
+int main(int argc, char **argv) {
+    FILE *f = fopen(argv[1], "rb");
+    fseek(f, 0, SEEK_END);
+    long n = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    unsigned char *buf = malloc(n ? n : 1);
+    if (fread(buf, 1, n, f) != (size_t)n) return 2;
+    fclose(f);
+    static const unsigned steps[] = {1, 7, 63, 64, 65, 1000, 4096};
+    for (int a = 2; a < argc; ++a) {
+        int L = atoi(argv[a]);
+        uint8_t d1[20], d2[20];
+        oracle_shahash(buf, L, d1);
+        oracle_sha1_ctx c;
+        oracle_sha1_init(&c);
+        for (int p = 0, k = 0; p < L; ++k) {
+            int s = (int)steps[k % 7];
+            if (s > L - p) s = L - p;
+            oracle_sha1_update(&c, buf + p, (uint32_t)s);
+            p += s;
+        }
+        oracle_sha1_final(&c, d2);
+        printf("%d ", L);
+        for (int i = 0; i < 20; ++i) printf("%02x", d1[i]);
+        printf(" ");
+        for (int i = 0; i < 20; ++i) printf("%02x", d2[i]);
+        printf("\n");
+    }
+    free(buf);
+    return 0;
+}
+'''
+
+_CHUNKFILE_DRV = r'''
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include "chunk_hash.h"
+typedef struct vector { int ele_size; int len; int size; void *val; } vector;
+void vec_add(vector *v, void *ele) {
+    if (v->size == v->len) { v->val = realloc(v->val, (size_t)v->ele_size * v->size * 2); v->size *= 2; }
+    memcpy((char *)v->val + (size_t)v->len * v->ele_size, ele, v->ele_size);
+    v->len++;
+}
+int main(int argc, char **argv) {
+    vector v = {45, 0, 2, malloc(90)};
+    read_chunk(argv[1], &v);
+    printf("N %d\n", v.len);
+    for (int q = 2; q < argc; ++q) printf("I %zd\n", (ssize_t)find_chunk_idx_from_hash(argv[q], argv[1]));
+    FILE *f = fopen(argv[1], "r");
+    seek_to_chunk_pos(f, 9000);
+    seek_to_packet_pos(f, 3, 7);
+    printf("S %lld\n", (long long)ftello(f));
+    fclose(f);
+    free(v.val);
+    return 0;
+}
+'''
+
+
+def _gcc(tmp_path, name, src, extra):
+    (tmp_path / f"{name}.c").write_text(src)
+    exe = tmp_path / name
+    r = subprocess.run(["gcc", *SAN, "-I", os.path.join(ROOT, "include"), *extra,
+                        str(tmp_path / f"{name}.c"), "-o", str(exe)], capture_output=True, text=True)
+    if r.returncode != 0 and "sanitizer" in r.stderr.lower():
+        pytest.skip("sanitizer runtime not available: " + r.stderr[-200:])
+    assert r.returncode == 0, r.stderr
+    return exe
+
+
+def test_oracle_under_asan_ubsan(tmp_path):
+    exe = _gcc(tmp_path, "odrv", _ORACLE_DRV,
+               ["-I", os.path.join(ROOT, "oracle"), os.path.join(ROOT, "oracle", "sha1_oracle.c"), "-lpthread"])
+    rng = np.random.default_rng(3)
+    data = rng.integers(0, 256, 200000, dtype=np.uint8).tobytes()
+    (tmp_path / "data.bin").write_bytes(data)
+    lens = list(range(0, 301)) + [4095, 4096, 4097, 65535, 131072, 199999]
+    r = subprocess.run([str(exe), str(tmp_path / "data.bin"), *map(str, lens)], capture_output=True,
+                       text=True, env=ENV)
+    assert r.returncode == 0, r.stderr[-2000:]
+    rows = r.stdout.split("\n")[:-1]
+    assert len(rows) == len(lens)
+    for row, L in zip(rows, lens):
+        l, one, streamed = row.split()
+        want = hashlib.sha1(data[:L]).hexdigest()
+        assert int(l) == L and one == want and streamed == want, L
+
+
+def test_chunk_file_readers_under_asan_ubsan(tmp_path):
+    exe = _gcc(tmp_path, "cdrv", _CHUNKFILE_DRV,
+               [os.path.join(ROOT, "congestion-control-with-bittorren_amd", "csrc", "chunk_file.c")])
+    hashes = [hashlib.sha1(bytes([i])).hexdigest() for i in range(5)]
+    files = {
+        "crlf": "".join(f"{i} {h}\r\n" for i, h in enumerate(hashes)),
+        "lf": "".join(f"{i} {h}\n" for i, h in enumerate(hashes)),
+        "comments": "# c\n0 " + hashes[0] + "\nnot a chunk\n7\n\n1 " + hashes[1] + "\n",
+        "master": f"File: /tmp/C.tar Chunks:0 {hashes[0]}\r\n" +
+                  "".join(f"{i} {h}\r\n" for i, h in enumerate(hashes) if i),
+        "empty": "",
+        "no_newline": f"0 {hashes[0]}",
+    }
+    for name, text in files.items():
+        p = tmp_path / f"{name}.chunks"
+        p.write_bytes(text.encode())
+        r = subprocess.run([str(exe), str(p), *hashes, "0" * 40], capture_output=True, text=True, env=ENV)
+        assert r.returncode == 0, (name, r.stderr[-2000:])
+        assert f"S {3 * 524288 + (1500 - 16) * 7}" in r.stdout
