@@ -1,0 +1,159 @@
+/* asan_driver.c -- test program, not part of the library: drives every
+ * host-side path of libsha1chunk (built with host AddressSanitizer +
+ * UndefinedBehaviorSanitizer, `make asan`) on a real device, so the runtime's
+ * host code -- pipelines, pinned staging, part pools, the verify queue, the
+ * streaming trio, the chunk-file C layer -- runs under the sanitizers.  GPU
+ * code is not instrumented (no GPU ASan on this pool).  Cross-checks the
+ * paths against each other and the NIST "abc" vector (sha.c:32-38); prints
+ * "asan-driver ok" and exits 0 when everything agrees.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include "../../include/chunk_hash.h"
+#include "../../include/sha.h"
+#include "../../include/sha1chunk.h"
+
+#define L512 524288u
+
+static int fails = 0;
+#define CHECK(c, ...)                                   \
+    do {                                                \
+        if (!(c)) {                                     \
+            fprintf(stderr, "FAIL %s:%d ", __FILE__, __LINE__); \
+            fprintf(stderr, __VA_ARGS__);               \
+            fprintf(stderr, "\n");                      \
+            ++fails;                                    \
+        }                                               \
+    } while (0)
+
+static uint64_t rng = 88172645463325252ull;
+static uint8_t next_byte(void) {
+    rng ^= rng << 13;
+    rng ^= rng >> 7;
+    rng ^= rng << 17;
+    return (uint8_t)rng;
+}
+
+int main(void) {
+    CHECK(sha1chunk_device_count() > 0, "no device: %s", sha1chunk_last_error());
+    /* NIST "abc" (sha.c:32-38) through shahash and the streaming trio */
+    static const uint8_t abc_want[20] = {0xa9, 0x99, 0x3e, 0x36, 0x47, 0x06, 0x81, 0x6a, 0xba, 0x3e,
+                                         0x25, 0x71, 0x78, 0x50, 0xc2, 0x6c, 0x9c, 0xd0, 0xd8, 0x9d};
+    uint8_t d[20], d2[20];
+    shahash((uint8_t *)"abc", 3, d);
+    CHECK(!memcmp(d, abc_want, 20), "shahash abc");
+    SHA1Context c;
+    SHA1Init(&c);
+    SHA1Update(&c, "a", 1);
+    SHA1Update(&c, "bc", 2);
+    SHA1Final(&c, d2);
+    CHECK(!memcmp(d2, abc_want, 20), "streaming abc");
+
+    /* ragged host batch: digests vs one shahash per chunk and vs streaming */
+    const size_t n = 300;
+    uint64_t *off = malloc(n * sizeof *off);
+    uint32_t *len = malloc(n * sizeof *len);
+    size_t total = 0;
+    for (size_t i = 0; i < n; ++i) {
+        len[i] = (i % 7 == 0) ? L512 : (uint32_t)((i * 7919u) % 70000u);
+        off[i] = total + (i % 3);
+        total = off[i] + len[i];
+    }
+    uint8_t *buf = malloc(total + 1);
+    for (size_t i = 0; i < total; ++i) buf[i] = next_byte();
+    uint8_t *dig = malloc(n * 20), *mis = malloc(n);
+    CHECK(sha1chunk_hash_batch(buf, off, len, n, dig, SHA1CHUNK_HOST) == 0, "hash_batch: %s",
+          sha1chunk_last_error());
+    for (size_t i = 0; i < n; i += 37) {
+        shahash(buf + off[i], (int)len[i], d);
+        CHECK(!memcmp(d, dig + 20 * i, 20), "batch vs shahash %zu", i);
+        SHA1Init(&c);
+        for (uint32_t p = 0; p < len[i];) {
+            uint32_t s = 1 + (p * 31u) % 5000u;
+            if (s > len[i] - p) s = len[i] - p;
+            SHA1Update(&c, buf + off[i] + p, s);
+            p += s;
+        }
+        SHA1Final(&c, d2);
+        CHECK(!memcmp(d2, dig + 20 * i, 20), "batch vs streaming %zu", i);
+    }
+    /* verify_batch with two corrupted expectations */
+    uint8_t *exp = malloc(n * 20);
+    memcpy(exp, dig, n * 20);
+    exp[20 * 5] ^= 1;
+    exp[20 * 200 + 19] ^= 0x80;
+    CHECK(sha1chunk_verify_batch(buf, off, len, n, exp, mis, SHA1CHUNK_HOST) == 0, "verify_batch");
+    for (size_t i = 0; i < n; ++i) CHECK(mis[i] == (i == 5 || i == 200), "verify_batch flag %zu", i);
+
+    /* verify queue: growth, polling, flush; every tag once with the right flag */
+    sha1chunk_vq *q = sha1chunk_vq_create(16, L512);
+    CHECK(q != NULL, "vq_create: %s", sha1chunk_last_error());
+    size_t seen = 0;
+    uint8_t *got = calloc(n, 1);
+    uint64_t tags[64];
+    uint8_t bad[64];
+    for (size_t i = 0; i < n; ++i) {
+        CHECK(sha1chunk_vq_submit(q, buf + off[i], len[i], exp + 20 * i, i) == 0, "vq_submit");
+        long k = sha1chunk_vq_poll(q, tags, bad, 64, 0);
+        for (long j = 0; j < k; ++j) {
+            CHECK(tags[j] < n && !got[tags[j]], "vq tag");
+            got[tags[j]] = 1;
+            CHECK(bad[j] == (tags[j] == 5 || tags[j] == 200), "vq flag %llu", (unsigned long long)tags[j]);
+            ++seen;
+        }
+    }
+    for (;;) {
+        long k = sha1chunk_vq_poll(q, tags, bad, 64, 1);
+        if (k <= 0) break;
+        for (long j = 0; j < k; ++j) {
+            CHECK(tags[j] < n && !got[tags[j]], "vq tag");
+            got[tags[j]] = 1;
+            CHECK(bad[j] == (tags[j] == 5 || tags[j] == 200), "vq flag");
+            ++seen;
+        }
+    }
+    CHECK(seen == n && sha1chunk_vq_pending(q) == 0, "vq drained %zu of %zu", seen, n);
+    sha1chunk_vq_destroy(q);
+
+    /* file pipeline: make_chunks(FILE*) and the fd path over a temp file */
+    char path[] = "/tmp/asan_driver_XXXXXX";
+    int fd = mkstemp(path);
+    const size_t fbytes = 9 * (size_t)L512 + 12345;
+    CHECK(fd >= 0 && write(fd, buf, fbytes) == (ssize_t)fbytes, "temp file");
+    close(fd);
+    FILE *f = fopen(path, "r");
+    uint8_t *hs[10];
+    for (int i = 0; i < 10; ++i) hs[i] = malloc(20);
+    int m = make_chunks(f, hs);
+    fclose(f);
+    CHECK(m == 10, "make_chunks count %d", m);
+    for (int i = 0; i < 10 && i < m; ++i) {
+        shahash(buf + (size_t)i * L512, i < 9 ? (int)L512 : 12345, d);
+        CHECK(!memcmp(d, hs[i], 20), "make_chunks chunk %d", i);
+        free(hs[i]);
+    }
+    char *hex = get_chunk_hash((char *)buf, L512);
+    char want_hex[41];
+    shahash(buf, L512, d);
+    binary2hex(d, 20, want_hex);
+    CHECK(!strcmp(hex, want_hex), "get_chunk_hash");
+    CHECK(verify_hash(hex, (char *)buf) == 0, "verify_hash match");
+    free(hex);
+    unlink(path);
+
+    free(off), free(len), free(buf), free(dig), free(mis), free(exp), free(got);
+    /* _exit: skip the HIP/HSA runtime's own teardown, which trips the ROCm
+     * ASan runtime's device-allocator check after main (not this code) */
+    if (fails) {
+        fprintf(stderr, "asan-driver: %d failures\n", fails);
+        fflush(NULL);
+        _exit(1);
+    }
+    printf("asan-driver ok\n");
+    fflush(NULL);
+    _exit(0);
+}

@@ -387,6 +387,21 @@ def test_host_batch_all_devices(pkg, dev, oracle, golden):
 
 
 # ------------------------------------------------------- verify queue ----
+def test_host_paths_under_asan(pkg, dev):
+    """Every host path of the library (batch pipelines, pinned staging, part
+    pools, verify queue with growth, streaming trio, make_chunks(FILE*),
+    get_chunk_hash/verify_hash) under host AddressSanitizer + UBSan
+    (`make asan`: csrc/asan_driver.c against build-asan/libsha1chunk.so,
+    built on the CPU beforehand like every other binary).  Device code is
+    not instrumented; any host report makes the driver exit non-zero."""
+    exe = os.path.join(PKG_DIR, "build-asan", "asan_driver")
+    assert os.path.exists(exe), "run `make -C congestion-control-with-bittorren_amd asan` first"
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:halt_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0 and "asan-driver ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
+
+
 _ALL_DEVICES_SCRIPT = r"""
 import hashlib, importlib, sys
 import numpy as np
