@@ -28,112 +28,12 @@
 #include <vector>
 
 #include "../../include/sha1chunk.h"
+#include "part_pool.hpp"
 #include "sha1_kernels.h"
 
 namespace {
-// Persistent helper threads that run the parts of one job (a host copy
-// split in pieces, a file read split over pread calls) together with the
-// calling thread.  run() returns when every part is done.  Between jobs the
-// helpers poll for the next one for a while (a caller streaming chunks or
-// file pieces comes back within microseconds) before sleeping, so a job does
-// not pay a thread start or a futex wake-up.
-class PartPool {
-public:
-    explicit PartPool(int helpers) {
-        for (int i = 0; i < helpers; ++i) th_.emplace_back([this] { loop(); });
-    }
-    ~PartPool() {
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            stop_.store(true);
-        }
-        cv_.notify_all();
-        for (auto& t : th_) t.join();
-    }
-    size_t width() const { return th_.size() + 1; }
-    // fn(i) for i in [0, parts), on the caller and the helpers
-    void run(size_t parts, const std::function<void(size_t)>& fn) {
-        if (parts <= 1 || th_.empty()) {
-            for (size_t i = 0; i < parts; ++i) fn(i);
-            return;
-        }
-        {
-            std::lock_guard<std::mutex> g(mu_);
-            fn_ = &fn;
-            parts_.store(parts);
-            left_.store(parts);
-            next_.store(0);
-            gen_.fetch_add(1);
-        }
-        // helpers still polling see gen_ at once; only sleeping ones need the
-        // (syscall) wake-up
-        if (sleepers_.load() > 0) cv_.notify_all();
-        work();
-        // the caller's own parts are done; wait for the helpers' parts
-        for (int spin = 0; left_.load() != 0 && spin < 200000; ++spin) __builtin_ia32_pause();
-        if (left_.load() != 0) {
-            std::unique_lock<std::mutex> g(mu_);
-            done_.wait(g, [this] { return left_.load() == 0; });
-        }
-    }
-
-private:
-    static constexpr int kSpin = 20000;  // pause loops (tens of microseconds)
-    void work() {
-        for (size_t i; (i = next_.fetch_add(1)) < parts_.load();) {
-            (*fn_)(i);
-            if (left_.fetch_sub(1) == 1) {
-                std::lock_guard<std::mutex> g(mu_);
-                done_.notify_all();
-            }
-        }
-    }
-    void loop() {
-        uint64_t seen = 0;
-        for (;;) {
-            int spin = 0;
-            while (gen_.load() == seen && !stop_.load() && spin++ < kSpin) __builtin_ia32_pause();
-            if (gen_.load() == seen && !stop_.load()) {
-                std::unique_lock<std::mutex> g(mu_);
-                sleepers_.fetch_add(1);
-                cv_.wait(g, [&] { return stop_.load() || gen_.load() != seen; });
-                sleepers_.fetch_sub(1);
-            }
-            if (stop_.load()) return;
-            {
-                // a job's fields are published under mu_
-                std::lock_guard<std::mutex> g(mu_);
-                seen = gen_.load();
-            }
-            work();
-        }
-    }
-    std::vector<std::thread> th_;
-    std::mutex mu_;
-    std::condition_variable cv_, done_;
-    std::atomic<uint64_t> gen_{0};
-    std::atomic<int> sleepers_{0};
-    std::atomic<bool> stop_{false};
-    const std::function<void(size_t)>* fn_ = nullptr;
-    std::atomic<size_t> parts_{0};
-    std::atomic<size_t> next_{0};
-    std::atomic<size_t> left_{0};
-};
-
-// memcpy split over a pool (pieces of >= 64 KiB)
-void pool_copy(PartPool& pool, uint8_t* dst, const uint8_t* src, size_t n) {
-    const size_t parts = std::min<size_t>(pool.width(), n / (size_t(64) << 10));
-    if (parts <= 1) {
-        memcpy(dst, src, n);
-        return;
-    }
-    pool.run(parts, [&](size_t i) {
-        const size_t a = n * i / parts, b = n * (i + 1) / parts;
-        memcpy(dst + a, src + a, b - a);
-    });
-}
-
-
+using s1host::PartPool;
+using s1host::pool_copy;
 thread_local std::string t_err;
 thread_local int t_dev = 0;
 
