@@ -326,6 +326,7 @@ constexpr int kVSkipWave2 = 64;
 // pair's producers share one of the other two SIMDs: waves 1 + 5 and 3 + 7.
 // kVCross swaps which producer SIMD serves which consumer.
 constexpr int kVLayout8 = 128;
+constexpr int kVSkipWave1 = 512;  // with kVSkipWave2: leave wave 1 empty instead of wave 2 (A/B)
 constexpr int kVCross = 256;
 template <int PAIRS, int V, int NPROD>
 constexpr int kSplitThreads = (V & kVLayout8) ? 512 : 64 * PAIRS * (1 + NPROD) + ((V & kVSkipWave2) ? 64 : 0);
@@ -445,8 +446,10 @@ __global__ __launch_bounds__((kSplitThreads<PAIRS, V, NPROD>)) void sha1_split_k
     int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if constexpr ((V & kVSkipWave2) != 0) {
         static_assert(NPROD == 2 && PAIRS == 1, "skip-wave layout is for two producers");
-        if (wave == 2) return;  // never joins a barrier: an ended wave is not waited for
-        if (wave == 3) wave = 2;
+        // kVSkipWave1 (A/B): wave 1 stays empty instead, producers on waves 2 and 3
+        constexpr int skip = (V & kVSkipWave1) ? 1 : 2;
+        if (wave == skip) return;  // never joins a barrier: an ended wave is not waited for
+        if (wave > skip) wave -= 1;
     }
     int pair = wave % PAIRS;
     bool producer = wave >= PAIRS;
@@ -695,6 +698,9 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
 #undef SPLIT_2P
     case 569:  // 500 + (kVWK | kVUnmask | kVSkipWave2): producers on waves 1 and 3
         hipLaunchKernelGGL((sha1_split_kernel<4, 1, 69, 2>), dim3(groups), dim3(256), 0, st, A);
+        break;
+    case 578:  // 577 with wave 1 empty (producers on waves 2 and 3), A/B
+        hipLaunchKernelGGL((sha1_split_kernel<4, 1, 77 | kVSkipWave1, 2>), dim3(groups), dim3(256), 0, st, A);
         break;
     case 577:  // 569 + kVRead10
         hipLaunchKernelGGL((sha1_split_kernel<4, 1, 77, 2>), dim3(groups), dim3(256), 0, st, A);

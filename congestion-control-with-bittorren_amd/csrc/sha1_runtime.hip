@@ -262,7 +262,7 @@ int split_unit(size_t n, int cus) {
     if (const char* e = getenv("SHA1CHUNK_SPLIT_UNIT")) {
         const int u = atoi(e);
         if ((u >= 1 && u <= 4) || (u >= 8 && u <= 12) || (u >= 20 && u <= 47) || (u >= 500 && u <= 507) ||
-            u == 569 || u == 577)
+            u == 569 || u == 577 || u == 578)
             return u;
     }
     const size_t groups = (n + 63) / 64;
