@@ -10,7 +10,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 KERNELS = ["lane", "fused", "split", "auto"]
-SPLIT_UNITS = [1, 2, 3, 4, 8, 9, 10, 11, 12, 505, 569, 577]
+SPLIT_UNITS = [1, 2, 3, 4, 8, 9, 10, 11, 12, 505, 569, 577, 578]
 
 
 def _lengths(rng, n):

@@ -633,7 +633,7 @@ def test_make_chunks_from_stream_position(pkg, dev, golden, fixture_files, tmp_p
     assert out == "".join(f"{i} {h}\n" for i, h in enumerate(exp)) + "eof 1\n"
 
 
-@pytest.mark.parametrize("unit", [1, 2, 3, 4, 8, 9, 10, 11, 12, 505, 569, 577])
+@pytest.mark.parametrize("unit", [1, 2, 3, 4, 8, 9, 10, 11, 12, 505, 569, 577, 578])
 def test_every_split_shape_ragged(pkg, dev, oracle, unit, monkeypatch):
     """Every split-kernel shape the library builds (SHA1CHUNK_SPLIT_UNIT
     forces it: unit sizes, multi-pair workgroups, two-producer layouts) on
