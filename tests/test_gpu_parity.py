@@ -121,6 +121,23 @@ def test_make_chunks_cli_reproduces_C_chunks(pkg, dev, golden, fixture_files, tm
     assert out == want  # tmp/C.chunks with CRLF stripped
 
 
+@pytest.mark.parametrize("size", [0, 1, L512 - 1, L512, L512 + 1, 2 * L512, 2 * L512 + 55])
+def test_make_chunks_file_sizes(pkg, dev, tmp_path, size):
+    """make_chunks (chunk.c:15-27) and the CLI (make_chunks.c) on files at
+    the chunk boundaries: an empty file has no chunks, a partial last chunk
+    is hashed at its true length.  Checked against hashlib."""
+    import hashlib
+    rng = np.random.default_rng(size)
+    data = rng.integers(0, 256, size, dtype=np.uint8).tobytes()
+    p = tmp_path / "f.bin"
+    p.write_bytes(data)
+    want = [hashlib.sha1(data[i:i + L512]).hexdigest() for i in range(0, size, L512)]
+    assert [d.hex() for d in pkg.make_chunks(str(p))] == want
+    out = subprocess.run([os.path.join(PKG_DIR, "make-chunks"), str(p)], capture_output=True,
+                         text=True, check=True).stdout
+    assert out == "".join(f"{i} {h}\n" for i, h in enumerate(want))
+
+
 def test_reference_make_chunks_main_dropin(pkg, dev, golden, fixture_files, tmp_path):
     """The reference's own make_chunks.c main, unmodified, linked without
     chunk.o/sha.o against libsha1chunk.so (oracle/Makefile `dropin`, built in
