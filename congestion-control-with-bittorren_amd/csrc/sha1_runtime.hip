@@ -230,10 +230,12 @@ int get_device(Device** out) {
 }
 
 // Pick the kernel for a batch of n chunks on a device with `cus` CUs
-// (crossovers measured on MI355X, DESIGN.md "Kernel selection"):
+// (crossovers measured on MI355X: profiles/sweep_r01.json,
+// split_2prod_sweep_r01.json; DESIGN.md section 5, kernel table):
 //  - up to 2 groups of 64 chunks per CU, each chunk's serial instruction
-//    stream is the bound: the split kernel (rounds-only consumer wave, its
-//    producer on another SIMD) is ~1.4x the fused kernel per chunk;
+//    stream is the bound: the split kernel (rounds-only consumer wave alone
+//    on its SIMD, two producer waves on others) is ~1.4x the fused kernel
+//    per chunk;
 //  - beyond that the SIMDs are busy and the split kernel's LDS hand-off and
 //    barriers cost more than they save: the fused kernel (schedule + rounds
 //    in one wave, 4 blocks of register prefetch) wins.
