@@ -204,6 +204,18 @@ int device_count() {
     return g_count;
 }
 
+// Streams and events of slots [0, n), created on first use (caller holds D.mu).
+int ensure_slots(Device& D, int n) {
+    for (int i = 0; i < n && i < kMaxSlots; ++i) {
+        Slot& s = D.slot[i];
+        if (s.stream) continue;
+        HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
+        HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    }
+    return SHA1CHUNK_OK;
+}
+
 // Acquire the calling thread's device (initialising it on first use).
 int get_device(Device** out) {
     if (device_count() <= 0) return fail(SHA1CHUNK_ENODEV, "%s", g_probe_err.c_str());
@@ -216,11 +228,12 @@ int get_device(Device** out) {
             hipDeviceProp_t pr;
             HIP_TRY(hipGetDeviceProperties(&pr, D.id));
             D.cus = pr.multiProcessorCount;
-            for (auto& s : D.slot) {
-                HIP_TRY(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-                HIP_TRY(hipEventCreateWithFlags(&s.done, hipEventDisableTiming));
-                HIP_TRY(hipEventCreateWithFlags(&s.copied, hipEventDisableTiming));
-            }
+            // Only slot 0 and the copy stream now: a stream costs ~20 ms to
+            // create (profiles/startup_r01.json), and a one-chunk caller
+            // (shahash, verify_hash, the CLI on a small file) needs no more.
+            // Other slots are made by ensure_slots() on first use.
+            int rc = ensure_slots(D, 1);
+            if (rc) return rc;
             HIP_TRY(hipStreamCreateWithFlags(&D.copy, hipStreamNonBlocking));
             D.ready.store(true, std::memory_order_release);
         }
@@ -452,6 +465,7 @@ int hash_host(const uint8_t* base, const uint64_t* offsets, const uint32_t* leng
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(D->mu);
     if ((rc = discard_in_flight(*D))) return rc;
+    if ((rc = ensure_slots(*D, 2))) return rc;
     // Longest first, so every wave of 64 gets near-equal lengths (a wave
     // runs as long as its longest lane); equal lengths keep caller order.
     std::vector<uint32_t> order(n);
@@ -667,6 +681,7 @@ long hash_stream_sized(sha1chunk_reader_fn reader, void* reader_ctx, sha1chunk_s
     std::lock_guard<std::mutex> lk(D->mu);
     if ((rc = discard_in_flight(*D))) return rc;
     const int nslots = stream_slots();
+    if ((rc = ensure_slots(*D, nslots))) return rc;
     size_t slot_bytes = stream_slot_bytes();
     if (size_hint) {
         const size_t L = SHA1CHUNK_CHUNK_LEN;
