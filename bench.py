@@ -12,11 +12,14 @@ collectives are the timing barrier and the max-over-ranks reduction.
 Prints ONE JSON line on rank 0 with `roofline` (dominant kernel vs the HBM
 peak, per-launch time from HIP events on the kernel's own stream; `traffic`
 from the committed rocprofv3 PMC pass, profiles/traffic_*.json),
-`serial_bound` (the per-chunk limit that actually binds this workload: SHA-1
-is serial inside a chunk and one wave issues one instruction per 4
-cycles, so 4096 chunks = 64 waves cannot fill 1024 SIMDs) and
-`cpu_baseline` (the reference sha.c, compiled from its sources into
-oracle/_ref, timed on this host's cores on the same chunks).
+`binding_limit` (the limit that actually binds the workload's regime: at
+<= 2 groups of 64 chunks per CU one chunk's serial instruction stream --
+SHA-1 is serial inside a chunk and one wave issues one instruction per 4
+cycles, so config 2's 4096 chunks = 64 waves cannot fill 1024 SIMDs -- and
+beyond that the SIMDs' VALU time), `valu_ceiling` (the
+chip's SHA-1 VALU ceiling in the roofline's GB/s) and `cpu_baseline` (the
+reference sha.c, compiled from its sources into oracle/_ref, timed on this
+host's cores on the same chunks).
 
 --streams P (default 1) keeps P independent batches in flight on P HIP
 streams (each its own 4096 distinct chunks); the default measures one batch
@@ -41,24 +44,42 @@ sys.path.insert(0, ROOT)
 METRIC = "GiB/s device-resident SHA-1 over 512KB chunks; % of HBM-read roofline"
 CHUNK_LEN = 524288  # constants.h:14
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
-# Per-chunk serial floor: a rounds-only wave needs 5 VALU per round x 80
-# rounds per 64-B block, and one wave issues one instruction per 4.0 cycles
-# (straight-line streams, tools/issue_probe.hip -> profiles/issue_r01.json;
-# looped microbenchmarks read 4.63 because of their loop branch) at the
-# ~2.4 GHz the chip holds at this occupancy.
+# Issue-floor models of the kernels.  Instruction
+# counts per 64-B block of each kernel's steady-state loop, read from the
+# compiled gfx950 ISA by tools/isa_mix.py (profiles/isa_mix_r02.json):
+#  * split kernel (<= 2 groups of 64 chunks per CU): the rounds-only consumer
+#    wave issues CONSUMER_INSTR_PER_BLOCK instructions per block (400 round
+#    VALU + 20 ds_read_b128 of the schedule + 5 feed-forward adds + scalars),
+#    and one wave issues one instruction per 4.0 cycles (straight-line
+#    streams: tools/issue_probe.hip -> profiles/issue_r01.json; the
+#    "vector-instruction ISSUE cost" row of MI355X_MICROARCH.md).  The floor
+#    is one chunk's serial chain: blocks x instructions x 4 cycles.
+#  * fused kernel (more groups): the SIMD's VALU time.  gfx950 SIMDs are 32
+#    lanes wide: a full-rate wave64 VALU op takes 2 cycles, the half-rate ones
+#    (v_alignbit, v_add3, v_perm, ...) 4 (tools/microbench.hip,
+#    profiles/microbench_ops_r01.json: ~1.1 vs ~1.9 ns).  Per block the fused
+#    loop has 400 half-rate + 221.75 full-rate VALU = 2043.5 SIMD cycles per
+#    wave of 64 chunks.
+CONSUMER_INSTR_PER_BLOCK = 427.75
 ROUND_VALU_PER_BLOCK = 400
-# The split consumer's whole per-block stream (400 round ops + 20 ds_read_b128
-# of the schedule + 5 feed-forward adds + waits/barrier scalars), counted in
-# the unrolled 8-block loop of the 4-block-unit kernel (`make isa`).
-CONSUMER_INSTR_PER_BLOCK = 428
+FUSED_SIMD_CYCLES_PER_BLOCK = 2043.5
 ISSUE_CYCLES = 4.0
-CLOCK_HZ = 2.4e9
-# VALU-int roofline: the algorithmic SHA-1 op count per 64-B
-# block (80 x 5 round ops + 64 x 3 schedule ops + 16 byte swaps + 5
-# feed-forward adds) against the chip's int32 lane-op rate, 256 CU x 4 SIMD
-# x 16 lanes x 2.4 GHz.
-VALU_OPS_PER_BLOCK = 613
-VALU_PEAK_TOPS = 256 * 4 * 16 * 2.4e9 / 1e12
+CLOCK_HZ = 2.4e9  # MI355X max engine clock; the chip holds it at config-2 occupancy
+SIMDS_PER_CU = 4
+NAMED_WORKLOADS = {4096: "BASELINE config 2", 32768: "config 4 shard, 1 of 8 GPUs",
+                   65536: "config 3 size, device-resident", 262144: "config 4 whole, one GPU"}
+
+
+def _regime(n: int, cus: int, kernel: str) -> str:
+    """The kernel `kernel` (or AUTO's choice, sha1_runtime.hip choose_kernel /
+    split_unit) for n chunks on `cus` CUs."""
+    groups = (n + 63) // 64
+    if kernel == "auto":
+        kernel = "split" if groups <= 2 * cus else "fused"
+    if kernel == "split":
+        return "split_u4_2prod" if groups <= cus else ("split_u2_8wave" if groups <= 2 * cus
+                                                        else "split_u1")
+    return kernel
 
 
 def parse():
@@ -161,9 +182,41 @@ def main():
     alg_bytes = n * (L + 20)  # per launch: every chunk byte read once + its digest
     achieved = alg_bytes / (kern_ms * 1e-3) / 1e9
     blocks = (L + 8) // 64 + 1  # SHA-1 compressions per chunk (sha.c:536-543 padding)
-    floor_ms = blocks * ROUND_VALU_PER_BLOCK * ISSUE_CYCLES / CLOCK_HZ * 1e3
-    valu_tops = n * blocks * VALU_OPS_PER_BLOCK / (kern_ms * 1e-3) / 1e12  # one chunk per lane
-    stream_ms = blocks * CONSUMER_INSTR_PER_BLOCK * ISSUE_CYCLES / CLOCK_HZ * 1e3
+    cus = torch.cuda.get_device_properties(dev).multi_processor_count
+    regime = _regime(n, cus, a.kernel)
+    groups = (n + 63) // 64
+    # VALU ceiling of the chip for SHA-1 (every SIMD busy with the fused
+    # kernel's op mix at the max clock), in the same GB/s as the roofline
+    valu_peak = cus * SIMDS_PER_CU * 64 * 64 / FUSED_SIMD_CYCLES_PER_BLOCK * CLOCK_HZ / 1e9
+    if regime.startswith("split"):
+        floor_ms = blocks * CONSUMER_INSTR_PER_BLOCK * ISSUE_CYCLES / CLOCK_HZ * 1e3
+        binding = {
+            "limit": "per-chunk serial instruction issue (SHA-1 is serial inside a chunk; "
+                     f"{groups} groups of 64 chunks on {cus * SIMDS_PER_CU} SIMDs)",
+            "kernel": regime, "floor_ms": round(floor_ms, 4), "achieved_ms": round(kern_ms, 4),
+            "frac": round(floor_ms / kern_ms, 4),
+            "model": f"{blocks} blocks x {CONSUMER_INSTR_PER_BLOCK} consumer instructions x "
+                     f"{ISSUE_CYCLES:g} cyc / 2.4 GHz (profiles/isa_mix_r02.json)",
+            "rounds_only_floor_ms": round(blocks * ROUND_VALU_PER_BLOCK * ISSUE_CYCLES
+                                          / CLOCK_HZ * 1e3, 4),
+        }
+    elif regime == "fused":
+        waves_per_simd = groups / (cus * SIMDS_PER_CU)
+        floor_ms = waves_per_simd * blocks * FUSED_SIMD_CYCLES_PER_BLOCK / CLOCK_HZ * 1e3
+        binding = {
+            "limit": "SIMD VALU issue (every SIMD busy)", "kernel": regime,
+            "floor_ms": round(floor_ms, 4), "achieved_ms": round(kern_ms, 4),
+            "frac": round(floor_ms / kern_ms, 4),
+            "model": f"{waves_per_simd:g} waves/SIMD x {blocks} blocks x "
+                     f"{FUSED_SIMD_CYCLES_PER_BLOCK} SIMD cycles / 2.4 GHz (400 half-rate x 4 + "
+                     "221.75 full-rate x 2 per block, profiles/isa_mix_r02.json); the chip "
+                     "holds ~2.05 GHz under this load (profiles/pmc_fused_131072_r01.json)",
+        }
+    else:  # forced lane kernel (per-lane loads, A/B and test path): not modelled
+        binding = {"limit": "not modelled", "kernel": regime, "achieved_ms": round(kern_ms, 4)}
+    label = f"{n} x {L} B chunks per GPU, device-resident"
+    if L == CHUNK_LEN and n in NAMED_WORKLOADS:
+        label += f" ({NAMED_WORKLOADS[n]})"
 
     result = {
         "metric": METRIC,
@@ -178,10 +231,12 @@ def main():
         "vs_baseline": None,
         "dtype": "u32",
         "data": "synthetic (splitmix64 corpus, SURVEY.md 8d), resident in HBM",
-        "config": {"workload": f"{n} x {L} B chunks per GPU, device-resident (BASELINE config 2)",
-                   "chunks_per_gpu": n, "chunk_bytes": L, "kernel": a.kernel, "streams": P,
+        "config": {"workload": label,
+                   "chunks_per_gpu": n, "chunk_bytes": L, "kernel": regime, "streams": P,
                    "parallelism": f"chunk-sharded x{world}, no collective"},
         "parity": parity,
+        # HBM is the metric's denominator (BASELINE.json), not the binding
+        # limit: see binding_limit and valu_ceiling
         "roofline": {
             "bound": "hbm",
             "achieved": round(achieved, 2),
@@ -191,20 +246,13 @@ def main():
             "traffic": _traffic(n, L),
             "kernel_ms": round(kern_ms, 4),
         },
-        "valu_roofline": {
-            "achieved": round(valu_tops, 3), "peak": round(VALU_PEAK_TOPS, 2),
-            "unit": "T int32 lane-ops/s", "frac": round(valu_tops / VALU_PEAK_TOPS, 4),
-            "ops_per_block": VALU_OPS_PER_BLOCK,
+        "valu_ceiling": {
+            "achieved": round(achieved, 2), "peak": round(valu_peak, 1), "unit": "GB/s",
+            "frac": round(achieved / valu_peak, 4),
+            "model": f"{cus * SIMDS_PER_CU} SIMDs x 64 chunks x 64 B per "
+                     f"{FUSED_SIMD_CYCLES_PER_BLOCK} SIMD cycles at 2.4 GHz",
         },
-        "serial_bound": {
-            "bound": "per-chunk serial VALU issue (rounds-only wave)",
-            "floor_ms": round(floor_ms, 4), "achieved_ms": round(kern_ms, 4),
-            "frac": round(floor_ms / kern_ms, 4),
-            "model": f"{blocks} blocks x {ROUND_VALU_PER_BLOCK} VALU x {ISSUE_CYCLES:g} cyc / 2.4 GHz",
-            "stream_floor_ms": round(stream_ms, 4), "stream_frac": round(stream_ms / kern_ms, 4),
-            "stream_model": f"{blocks} blocks x {CONSUMER_INSTR_PER_BLOCK} consumer instructions "
-                            f"x {ISSUE_CYCLES:g} cyc / 2.4 GHz",
-        },
+        "binding_limit": binding,
     }
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle import oracle as O  # the CPU baseline leg only: the reference sha.c, timed

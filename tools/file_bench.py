@@ -69,7 +69,12 @@ def main():
     ap.add_argument("--tail", type=int, default=123457, help="extra bytes: a short last chunk")
     ap.add_argument("--out", default="")
     ap.add_argument("--reps", type=int, default=3, help="timed runs (median reported)")
+    ap.add_argument("--cli-slot-ab", default="",
+                    help="e.g. 128,512: only time the make-chunks CLI with each "
+                         "SHA1CHUNK_STREAM_SLOT_MIB, interleaved, and check every digest")
     a = ap.parse_args()
+    if a.cli_slot_ab:
+        return cli_slot_ab(a)
     pkg = importlib.import_module("congestion-control-with-bittorren_amd")
     size = int(a.gib * 2**30) + a.tail
     fd, path = tempfile.mkstemp(prefix="sha1bench_", suffix=".dat")
@@ -121,6 +126,54 @@ def main():
                "stream_piece_mib": os.environ.get("SHA1CHUNK_STREAM_PIECE_MIB", "default"),
                "page_cache_read_GiBps": round(read_gibs, 3),
                "pinned_h2d_GiBps": round(h2d, 3), "digests_spot_checked_ok": bool(ok)}
+        print(json.dumps(row), flush=True)
+        if a.out:
+            json.dump(row, open(a.out, "w"), indent=1)
+        if not ok:
+            sys.exit(1)
+    finally:
+        os.unlink(path)
+
+
+def cli_slot_ab(a) -> None:
+    """The make-chunks CLI's slot-size choice (make_chunks_main.c: 128 MiB
+    below 16 GiB, 512 MiB above) measured around the cutoff: each slot size
+    in turn, interleaved over the reps, on the same page-cached file; every
+    digest line checked against hashlib (16 threads)."""
+    from concurrent.futures import ThreadPoolExecutor
+    size = int(a.gib * 2**30) + a.tail
+    nchunks = (size + L - 1) // L
+    fd, path = tempfile.mkstemp(prefix="sha1bench_", suffix=".dat")
+    os.close(fd)
+    exe = os.path.join(ROOT, "congestion-control-with-bittorren_amd", "make-chunks")
+    slots = [int(x) for x in a.cli_slot_ab.split(",")]
+    try:
+        write_file(path, size)
+        read_rate(path)  # page cache warm
+
+        def sha(i):
+            with open(path, "rb") as f:
+                f.seek(i * L)
+                return hashlib.sha1(f.read(L)).hexdigest()
+
+        with ThreadPoolExecutor(16) as ex:
+            want = "".join(f"{i} {h}\n" for i, h in enumerate(ex.map(sha, range(nchunks))))
+        times = {m: [] for m in slots}
+        ok = True
+        for _ in range(a.reps):
+            for m in slots:
+                env = dict(os.environ, SHA1CHUNK_STREAM_SLOT_MIB=str(m))
+                t0 = time.perf_counter()
+                out = subprocess.run([exe, path], capture_output=True, text=True, check=True,
+                                     env=env).stdout
+                times[m].append(time.perf_counter() - t0)
+                ok &= out == want
+                print(f"slot {m} MiB: {times[m][-1]:.3f} s", flush=True)
+        row = {"file_bytes": size, "chunks": nchunks, "reps": a.reps,
+               "cli_seconds": {str(m): [round(t, 3) for t in v] for m, v in times.items()},
+               "cli_median_GiBps": {str(m): round(size / float(np.median(v)) / 2**30, 3)
+                                    for m, v in times.items()},
+               "all_digests_match_hashlib": bool(ok)}
         print(json.dumps(row), flush=True)
         if a.out:
             json.dump(row, open(a.out, "w"), indent=1)

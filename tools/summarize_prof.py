@@ -2,7 +2,13 @@
 """Summarise a tools/profile_bench.sh run (gpurun_out/prof_<tag>) into
 profiles/: the rocprofv3 kernel stats CSV as-is, the SQ counter CSV, and a
 traffic JSON (FETCH_SIZE x 2 gfx950 correction + WRITE_SIZE, per dispatch of
-the dominant kernel) that bench.py reads for roofline.traffic."""
+the dominant kernel) that bench.py reads for roofline.traffic.
+
+The x 2 read correction is measured, not quoted: tools/fetch_calib.hip reads
+a known 2 GiB both coalesced and in the hash kernels' own pattern (lane =
+chunk, 16-byte loads, 128 bytes per lane per stage) and FETCH_SIZE comes out
+at half the bytes in both (read bytes / FETCH_SIZE bytes = 1.99999 and
+1.99996), WRITE_SIZE at exactly the bytes written (profiles/fetch_calib_r02.json)."""
 import csv
 import json
 import os
@@ -39,9 +45,9 @@ rec = {
               "(tools/profile_bench.sh)",
     "kernel": k, "chunks": n, "chunk_bytes": L, "dispatches": len(fetch),
     "fetch_size_kb_per_dispatch": f_kb, "write_size_kb_per_dispatch": w_kb,
-    "correction": "gfx950 FETCH_SIZE reports half the bytes of a wide streaming read "
-                  "(MI355X_MICROARCH.md HBM section): read bytes = 2 x FETCH_SIZE x 1024; "
-                  "WRITE_SIZE x 1024 exact",
+    "correction": "gfx950 FETCH_SIZE reports half the bytes read in this access pattern "
+                  "(calibrated on a known 2 GiB read: profiles/fetch_calib_r02.json): read "
+                  "bytes = 2 x FETCH_SIZE x 1024; WRITE_SIZE x 1024 exact",
     "read_bytes_per_launch": rd, "write_bytes_per_launch": wr, "bytes_per_launch": rd + wr,
     "algorithmic_bytes_per_launch": alg, "traffic_over_algorithmic": (rd + wr) / alg,
 }
