@@ -31,11 +31,15 @@ int main(int argc, char *argv[]) {
     }
     const long long nchunks = ((long long)st.st_size + BT_CHUNK_SIZE - 1) / BT_CHUNK_SIZE;
     /* A one-shot process pins its pipeline ring once and never reuses it
-     * (~0.19 s per GiB pinned, profiles/startup_r01.json): below 16 GiB of
-     * input, 128 MiB slots finish sooner than the library's 512 MiB default
-     * (8 GiB file: 0.72 vs 0.96 s, profiles/file_vq_r01.json).  An explicit
+     * (~0.1-0.2 s per GiB pinned, profiles/init_cost_r02.jsonl), so smaller
+     * slots start sooner, while 512 MiB slots stream ~8 % faster per GiB.
+     * Measured through this CLI on page-cached files (tools/file_bench.py
+     * --cli-slot-ab, profiles/cli_slot_r02.json): 128 MiB slots are ahead by
+     * a constant ~0.3 s at 8, 16 and 24 GiB (0.67 / 0.83 / 1.05 s against
+     * 0.99 / 1.14 / 1.33 s, medians of 3), and the per-GiB slopes (0.0234 vs
+     * 0.0218 s/GiB) put the crossover near 190 GiB.  An explicit
      * SHA1CHUNK_STREAM_SLOT_MIB wins. */
-    setenv("SHA1CHUNK_STREAM_SLOT_MIB", st.st_size < (16LL << 30) ? "128" : "512", 0);
+    setenv("SHA1CHUNK_STREAM_SLOT_MIB", st.st_size < (192LL << 30) ? "128" : "512", 0);
     uint8_t **hashes = (uint8_t **)malloc((size_t)(nchunks > 0 ? nchunks : 1) * sizeof *hashes);
     uint8_t *store = (uint8_t *)malloc((size_t)(nchunks > 0 ? nchunks : 1) * SHA1_HASH_SIZE);
     if (hashes == NULL || store == NULL) {

@@ -24,8 +24,12 @@ struct BatchArgs {
 
 hipError_t launch_lane(const BatchArgs& A, hipStream_t st);
 hipError_t launch_fused(const BatchArgs& A, hipStream_t st);
-// unit_blocks 1..4: schedule blocks per producer/consumer barrier (LDS = unit_blocks * 40 KiB);
-// 8, 9: multi-pair workgroups; 10*U+V: variant flags (sha1_kernels.hip)
+// Split-kernel shapes (sha1_kernels.hip launch_split): 1 (1-block units), 4
+// (4-block units, two producers: <= 1 group per CU), 11 (8-wave workgroup of
+// two pairs: <= 2 groups per CU).  The A/B library (`make ab`,
+// -DSHA1CHUNK_AB_VARIANTS) also builds the study's other shapes and variant
+// flags (2, 3, 8-10, 12, 10*U+V, 500+V, 569, 577, 578).
+bool split_unit_built(int unit_blocks);
 hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st);
 hipError_t launch_synth(uint8_t* dst, const uint64_t* off, const uint32_t* lens, uint32_t ulen,
                         uint64_t first, uint64_t count, uint64_t seed, hipStream_t st);

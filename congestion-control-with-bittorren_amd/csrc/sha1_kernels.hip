@@ -668,18 +668,42 @@ hipError_t launch_fused(const BatchArgs& A, hipStream_t st) {
     return hipGetLastError();
 }
 
+bool split_unit_built(int u) {
+#ifdef SHA1CHUNK_AB_VARIANTS
+    static const int built[] = {1,  2,  3,  4,  8,  9,  10, 11, 12, 20, 21, 22, 23, 24, 26, 27,
+                                30, 31, 32, 33, 34, 36, 37, 42, 44, 45, 46, 504, 505, 506, 507,
+                                569, 577, 578};
+    for (int b : built)
+        if (u == b) return true;
+    return false;
+#else
+    return u == 1 || u == 4 || u == 11;
+#endif
+}
+
 hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     if (A.n == 0) return hipSuccess;
     const uint32_t groups = (A.n + 63u) / 64u;
     switch (unit_blocks) {
     case 1: hipLaunchKernelGGL((sha1_split_kernel<1, 1>), dim3(groups), dim3(128), 0, st, A); break;
-    case 2: hipLaunchKernelGGL((sha1_split_kernel<2, 1>), dim3(groups), dim3(128), 0, st, A); break;
-    case 3: hipLaunchKernelGGL((sha1_split_kernel<3, 1>), dim3(groups), dim3(128), 0, st, A); break;
     case 4:  // two producers per consumer (kSplitNProd<4>), wave 2 empty: 256 threads
         hipLaunchKernelGGL((sha1_split_kernel<4, 1, kSplitV<4>, kSplitNProd<4>>), dim3(groups),
                            dim3(64 * (1 + kSplitNProd<4>) + ((kSplitV<4> & kVSkipWave2) ? 64 : 0)), 0,
                            st, A);
         break;
+    case 11:  // <= 2 groups per CU: 2 pairs x (consumer + 2 producers), 2-block
+              // units, 8-wave layout, producer SIMDs crossed between the pairs
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, kVWK | kVUnmask | kVLayout8 | kVCross, 2>),
+                           dim3((groups + 1) / 2), dim3(512), 0, st, A);
+        break;
+#ifdef SHA1CHUNK_AB_VARIANTS
+    // The shapes and variants of the split-kernel study (profiles/sweep_r01.json,
+    // split_variants_r01.json, split_2prod_sweep_r01.json), built only into
+    // the A/B library (`make ab` -> build-ab/libsha1chunk.so, selected with
+    // SHA1CHUNK_LIB): each instantiation is ~100 KiB of code object that a
+    // short-lived caller would otherwise load on its first launch.
+    case 2: hipLaunchKernelGGL((sha1_split_kernel<2, 1>), dim3(groups), dim3(128), 0, st, A); break;
+    case 3: hipLaunchKernelGGL((sha1_split_kernel<3, 1>), dim3(groups), dim3(128), 0, st, A); break;
 #define SPLIT_V(U, V)                                                                             \
     case 10 * U + V:                                                                              \
         hipLaunchKernelGGL((sha1_split_kernel<U, 1, V>), dim3(groups), dim3(128), 0, st, A);   \
@@ -713,10 +737,6 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
         hipLaunchKernelGGL((sha1_split_kernel<2, 2, kVWK | kVUnmask | kVLayout8, 2>), dim3((groups + 1) / 2),
                            dim3(512), 0, st, A);
         break;
-    case 11:  // case 10 with the producer SIMDs swapped between the pairs
-        hipLaunchKernelGGL((sha1_split_kernel<2, 2, kVWK | kVUnmask | kVLayout8 | kVCross, 2>),
-                           dim3((groups + 1) / 2), dim3(512), 0, st, A);
-        break;
     case 12:  // case 10 with schedule reads in bursts of 10
         hipLaunchKernelGGL((sha1_split_kernel<2, 2, kVWK | kVUnmask | kVLayout8 | kVRead10, 2>),
                            dim3((groups + 1) / 2), dim3(512), 0, st, A);
@@ -724,6 +744,7 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     case 9:  // 2 pairs per workgroup, 2-block units
         hipLaunchKernelGGL((sha1_split_kernel<2, 2>), dim3((groups + 1) / 2), dim3(256), 0, st, A);
         break;
+#endif
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();

@@ -269,17 +269,13 @@ int choose_kernel(int kernel, size_t n, int cus) {
 // CU one 8-wave workgroup holding both, 2-block units, two producers per
 // consumer sharing a SIMD and each consumer alone on its own (case 11:
 // 10-11 % faster than two 2-wave workgroups, profiles/split_2prod_sweep_r01.json);
-// else 1-block units (40 KiB).  SHA1CHUNK_SPLIT_UNIT overrides for A/B runs
-// (1..4 units, 8/9 multi-pair shapes, 10*U+V single-producer variants,
-// 500+V / 569 / 577 two-producer 4-block variants, 10-12 two pairs with two
-// producers each; see launch_split).
+// else 1-block units (40 KiB).  SHA1CHUNK_SPLIT_UNIT forces a shape for A/B
+// runs: 1, 4, 11 in the product library; the study's other shapes and
+// variants only in the A/B library (`make ab`, sha1_kernels.h).  Forcing a
+// shape this library does not hold fails the call (SHA1CHUNK_EINVAL,
+// launch_checked) instead of timing some other kernel.
 int split_unit(size_t n, int cus) {
-    if (const char* e = getenv("SHA1CHUNK_SPLIT_UNIT")) {
-        const int u = atoi(e);
-        if ((u >= 1 && u <= 4) || (u >= 8 && u <= 12) || (u >= 20 && u <= 47) || (u >= 500 && u <= 507) ||
-            u == 569 || u == 577 || u == 578)
-            return u;
-    }
+    if (const char* e = getenv("SHA1CHUNK_SPLIT_UNIT")) return atoi(e);
     const size_t groups = (n + 63) / 64;
     if (groups <= size_t(cus)) return 4;
     if (groups <= size_t(cus) * 2) return 11;
@@ -302,6 +298,9 @@ int launch_checked(int kernel, const BatchArgs& A, hipStream_t st, int cus = 256
         return fail(SHA1CHUNK_EINVAL, "batch of %u chunks: at most 2^32 - 1025 per call", A.n);
     if (A.n > 0 && (reinterpret_cast<uintptr_t>(A.dig) & 3u))
         return fail(SHA1CHUNK_EALIGN, "digest buffer must be 4-byte aligned");
+    if (kernel == SHA1CHUNK_KERNEL_SPLIT && !split_unit_built(split_unit(A.n, cus)))
+        return fail(SHA1CHUNK_EINVAL, "split shape %d is not in this library (A/B shapes: `make ab`)",
+                    split_unit(A.n, cus));
     hipError_t e = launch(kernel, A, cus, st);
     if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "kernel launch: %s", hipGetErrorString(e));
     return SHA1CHUNK_OK;

@@ -28,7 +28,9 @@ from typing import Iterable, Sequence
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsha1chunk.so")
+# SHA1CHUNK_LIB selects another build of the library (the A/B build,
+# `make ab` -> build-ab/libsha1chunk.so, for tools/sweep.py-style studies)
+LIB_PATH = os.environ.get("SHA1CHUNK_LIB") or os.path.join(HERE, "libsha1chunk.so")
 CHUNK_LEN = 524288  # constants.h:14
 DIGEST_LEN = 20
 SEED = 0x5EED0001

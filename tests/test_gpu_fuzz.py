@@ -12,7 +12,7 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 KERNELS = ["lane", "fused", "split", "auto"]
-SPLIT_UNITS = [1, 2, 3, 4, 8, 9, 10, 11, 12, 505, 569, 577, 578]
+SPLIT_UNITS = [1, 4, 11]  # the product library's split shapes
 
 
 def _lengths(rng, n):
