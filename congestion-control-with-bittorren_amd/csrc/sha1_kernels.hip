@@ -700,8 +700,9 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     // The shapes and variants of the split-kernel study (profiles/sweep_r01.json,
     // split_variants_r01.json, split_2prod_sweep_r01.json), built only into
     // the A/B library (`make ab` -> build-ab/libsha1chunk.so, selected with
-    // SHA1CHUNK_LIB): each instantiation is ~100 KiB of code object that a
-    // short-lived caller would otherwise load on its first launch.
+    // SHA1CHUNK_LIB).  The product library holds only what AUTO dispatches:
+    // 1.8 instead of 3.3 MiB of code object (start-up measured the same
+    // either way, profiles/startup_r02.json).
     case 2: hipLaunchKernelGGL((sha1_split_kernel<2, 1>), dim3(groups), dim3(128), 0, st, A); break;
     case 3: hipLaunchKernelGGL((sha1_split_kernel<3, 1>), dim3(groups), dim3(128), 0, st, A); break;
 #define SPLIT_V(U, V)                                                                             \
