@@ -60,6 +60,12 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 #    profiles/microbench_ops_r01.json: ~1.1 vs ~1.9 ns).  Per block the fused
 #    loop has 400 half-rate + 221.75 full-rate VALU = 2043.5 SIMD cycles per
 #    wave of 64 chunks.
+# Measured counterpart of that model: the same compression on register data
+# with no memory traffic, every SIMD holding 8 waves, reaches 3940 GB/s of
+# message bytes (tools/microbench.hip compress_test "512 x 1024",
+# profiles/microbench_issue_r01.json): the chip lowers its clock under a
+# full VALU load, so this, not the 2.4 GHz model, is what a kernel can reach.
+COMPRESS_ONLY_GBS = 3939.8
 CONSUMER_INSTR_PER_BLOCK = 427.75
 ROUND_VALU_PER_BLOCK = 400
 FUSED_SIMD_CYCLES_PER_BLOCK = 2043.5
@@ -251,6 +257,8 @@ def main():
             "frac": round(achieved / valu_peak, 4),
             "model": f"{cus * SIMDS_PER_CU} SIMDs x 64 chunks x 64 B per "
                      f"{FUSED_SIMD_CYCLES_PER_BLOCK} SIMD cycles at 2.4 GHz",
+            "measured_compress_only": COMPRESS_ONLY_GBS,
+            "frac_of_measured": round(achieved / COMPRESS_ONLY_GBS, 4),
         },
         "binding_limit": binding,
     }
