@@ -328,6 +328,10 @@ constexpr int kVSkipWave2 = 64;
 constexpr int kVLayout8 = 128;
 constexpr int kVSkipWave1 = 512;  // with kVSkipWave2: leave wave 1 empty instead of wave 2 (A/B)
 constexpr int kVCross = 256;
+// Round-2 A/B flags (A/B library only): consumer at s_setprio 3; all 20
+// schedule reads of the next block in one burst before round 0.
+constexpr int kVPrio = 2048;
+constexpr int kVRead20 = 4096;
 template <int PAIRS, int V, int NPROD>
 constexpr int kSplitThreads = (V & kVLayout8) ? 512 : 64 * PAIRS * (1 + NPROD) + ((V & kVSkipWave2) ? 64 : 0);
 // Why W+K matters: the consumer's x = e + W + K as a VOP3 v_add3 (K in an
@@ -366,7 +370,14 @@ __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (
     }
     if constexpr (jn == 0) split_barrier();
     uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
-    if constexpr ((V & kVRead10) != 0) {
+    if constexpr ((V & kVRead20) != 0) {
+        read_w_group<0>(slot, Wn);
+        read_w_group<1>(slot, Wn);
+        read_w_group<2>(slot, Wn);
+        read_w_group<3>(slot, Wn);
+        __builtin_amdgcn_sched_barrier(0);
+        RoundsW<0, 80, WK>::run(v, Wc);
+    } else if constexpr ((V & kVRead10) != 0) {
         // two bursts of 10 reads (before rounds 0 and 40)
         read_w_group<0>(slot, Wn);
         read_w_group<1>(slot, Wn);
@@ -550,6 +561,7 @@ __global__ __launch_bounds__((kSplitThreads<PAIRS, V, NPROD>)) void sha1_split_k
         uint32_t h[5];
         load_init(A, en.id, h);
         uint32_t Wa[80], Wb[80];
+        if constexpr ((V & kVPrio) != 0) __builtin_amdgcn_s_setprio(3);
         split_barrier();  // B_0
         read_w_group<0>(ring + lane * 16, Wa);
         read_w_group<1>(ring + lane * 16, Wa);
@@ -672,7 +684,7 @@ bool split_unit_built(int u) {
 #ifdef SHA1CHUNK_AB_VARIANTS
     static const int built[] = {1,  2,  3,  4,  8,  9,  10, 11, 12, 20, 21, 22, 23, 24, 26, 27,
                                 30, 31, 32, 33, 34, 36, 37, 42, 44, 45, 46, 504, 505, 506, 507,
-                                569, 577, 578};
+                                569, 577, 578, 579, 580, 581};
     for (int b : built)
         if (u == b) return true;
     return false;
@@ -729,6 +741,17 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
         break;
     case 577:  // 569 + kVRead10
         hipLaunchKernelGGL((sha1_split_kernel<4, 1, 77, 2>), dim3(groups), dim3(256), 0, st, A);
+        break;
+    case 579:  // 577 + consumer at s_setprio 3
+        hipLaunchKernelGGL((sha1_split_kernel<4, 1, 77 | kVPrio, 2>), dim3(groups), dim3(256), 0, st, A);
+        break;
+    case 580:  // 577 with all 20 reads in one burst
+        hipLaunchKernelGGL((sha1_split_kernel<4, 1, (77 & ~kVRead10) | kVRead20, 2>), dim3(groups),
+                           dim3(256), 0, st, A);
+        break;
+    case 581:  // 580 + s_setprio 3
+        hipLaunchKernelGGL((sha1_split_kernel<4, 1, (77 & ~kVRead10) | kVRead20 | kVPrio, 2>),
+                           dim3(groups), dim3(256), 0, st, A);
         break;
 
     case 8:  // 4 pairs per workgroup (512 threads), one consumer + producer per SIMD
