@@ -10,8 +10,8 @@
 //
 // How it maps to CDNA4 (one SHA-1 message per lane; 64 messages per wave):
 //   rotate            -> v_alignbit_b32 (1 op)
-//   Ch                -> v_bfi_b32 (compiler pattern)  Parity/Maj -> v_bitop3_b32
-//   5-term round sum  -> 2 x v_add3_u32
+//   Ch/Parity/Maj     -> v_bitop3_b32 (one op each)
+//   5-term round sum  -> 2 x v_add3_u32 (split consumer: v_add + v_add3)
 //   schedule xor4     -> v_bitop3_b32(xor3) + v_xor_b32, then v_alignbit_b32
 //   byte swap         -> v_perm_b32
 // = ~613 VALU per 64-byte block, no MFMA, no LDS inside the compression.
@@ -35,12 +35,12 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 __device__ __forceinline__ uint32_t maj(uint32_t a, uint32_t b, uint32_t c) {
     return __builtin_amdgcn_bitop3_b32(a, b, c, 0xE8);
 }
-// Ch = b ? c : d -> v_bfi_b32 (compiler pattern).  v_bitop3 (table 0xCA) is
-// also one VALU and in the faster SIMD-time class, but measured A/B on
-// MI355X it made the split consumer 3% slower (7.06 vs 6.85 ms at 4096
-// chunks: hipcc schedules the Ch right before its add3 and bitop3's result
-// latency is not hidden by one wave) and left the fused kernel unchanged
-// (profiles/ch_bitop3_ab_r01.json).
+// Ch = b ? c : d.  Written as d ^ (b & (c ^ d)), which hipcc folds into one
+// v_bitop3_b32 in every shipped kernel (profiles/isa_mix_r02.json: 80
+// bitop3 per block in the consumer, no v_bfi).  Round 1 measured forcing the
+// bitop3 through the builtin 3% slower in the consumer, because of where
+// hipcc then scheduled it (profiles/ch_bitop3_ab_r01.json); this form lets
+// the compiler place it.
 __device__ __forceinline__ uint32_t chf(uint32_t b, uint32_t c, uint32_t d) {
     return d ^ (b & (c ^ d));
 }
@@ -56,7 +56,20 @@ __device__ __forceinline__ constexpr uint32_t round_k() {
 
 // WK = true: wt already holds W[t] + K[t] (the split producer adds it), so
 // e + W + K is a 2-operand v_add_u32 (VOP2, issues ~6% faster than VOP3).
-template <int T, bool WK = false>
+// RV (A/B, fused kernel): 0 = the sums as two v_add3_u32 (half-rate); 1 =
+// every sum as full-rate VOP2 v_add_u32 (four per round, K as a literal);
+// 2 = e + W + K as two VOP2 adds, the round sum still one add3.
+__device__ __forceinline__ uint32_t add_vop2(uint32_t a, uint32_t b) {
+    uint32_t r;
+    asm("v_add_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
+    return r;
+}
+__device__ __forceinline__ uint32_t add_vop2_k(uint32_t a, uint32_t k) {
+    uint32_t r;
+    asm("v_add_u32 %0, %2, %1" : "=v"(r) : "v"(a), "i"(k));
+    return r;
+}
+template <int T, bool WK = false, int RV = 0>
 __device__ __forceinline__ void round_step(uint32_t (&v)[5], uint32_t wt) {
     constexpr int ia = (5 - (T % 5)) % 5;
     constexpr int ib = (ia + 1) % 5, ic = (ia + 2) % 5, id = (ia + 3) % 5, ie = (ia + 4) % 5;
@@ -77,10 +90,15 @@ __device__ __forceinline__ void round_step(uint32_t (&v)[5], uint32_t wt) {
     uint32_t x;
     if constexpr (WK)
         x = v[ie] + wt;
+    else if constexpr (RV != 0)
+        x = add_vop2_k(add_vop2(v[ie], wt), round_k<T>());
     else
         x = v[ie] + wt + round_k<T>();
     uint32_t t;
-    asm("v_add3_u32 %0, %1, %2, %3" : "=v"(t) : "v"(rotl(v[ia], 5)), "v"(f), "v"(x));
+    if constexpr (RV == 1)
+        t = add_vop2(add_vop2(rotl(v[ia], 5), f), x);
+    else
+        asm("v_add3_u32 %0, %1, %2, %3" : "=v"(t) : "v"(rotl(v[ia], 5)), "v"(f), "v"(x));
     v[ie] = t;
     v[ib] = rotl(v[ib], 30);
 }
@@ -93,28 +111,27 @@ __device__ __forceinline__ uint32_t sched_step(uint32_t (&w)[16]) {
     return x;
 }
 
-template <int T>
+template <int T, int RV = 0>
 struct Rounds {
     __device__ __forceinline__ static void run(uint32_t (&v)[5], uint32_t (&w)[16]) {
-        uint32_t wt;
-        if constexpr (T < 16)
-            wt = w[T];
-        else
-            wt = sched_step<T>(w);
-        round_step<T>(v, wt);
-        Rounds<T + 1>::run(v, w);
+        if constexpr (T < 80) {
+            uint32_t wt;
+            if constexpr (T < 16)
+                wt = w[T];
+            else
+                wt = sched_step<T>(w);
+            round_step<T, false, RV>(v, wt);
+            Rounds<T + 1, RV>::run(v, w);
+        }
     }
-};
-template <>
-struct Rounds<80> {
-    __device__ __forceinline__ static void run(uint32_t (&)[5], uint32_t (&)[16]) {}
 };
 
 // One full compression: h[] <- h[] + F(h[], w[]); w[] holds the block as
 // big-endian words and is consumed (overwritten by the schedule).
+template <int RV = 0>
 __device__ __forceinline__ void compress(uint32_t (&h)[5], uint32_t (&w)[16]) {
     uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
-    Rounds<0>::run(v, w);
+    Rounds<0, RV>::run(v, w);
 #pragma unroll
     for (int i = 0; i < 5; ++i) h[i] += v[i];
 }

@@ -589,6 +589,7 @@ __global__ __launch_bounds__((kSplitThreads<PAIRS, V, NPROD>)) void sha1_split_k
 // kernel's LDS hand-off is pure overhead.  Each lane streams its own chunk
 // with 16-byte loads, two 128-byte stages (4 blocks) in flight in VGPRs so
 // HBM latency under full load stays covered.
+template <int RV>
 __device__ __forceinline__ void fused_stage(uint32_t s, uint32_t S, const Entry& en, Stage& cur,
                                             uint32_t (&h)[5]) {
 #pragma unroll
@@ -597,10 +598,13 @@ __device__ __forceinline__ void fused_stage(uint32_t s, uint32_t S, const Entry&
 #pragma unroll
         for (int j = 0; j < 16; ++j) w[j] = bswap(cur.w[16 * half + j]);
         if (half == 1 && s + 2 < S) load_stage(en.p + 128ull * (s + 2), cur);
-        compress(h, w);
+        compress<RV>(h, w);
     }
 }
 
+// RV: round-sum form (sha1_device.hpp round_step); the product uses 0, the
+// A/B library also builds 1 and 2 (SHA1CHUNK_FUSED_VARIANT).
+template <int RV = 0>
 __global__ __launch_bounds__(256) void sha1_fused_kernel(BatchArgs A) {
     const uint32_t e = blockIdx.x * 256u + threadIdx.x;
     const uint32_t group = e / 64u;
@@ -619,10 +623,10 @@ __global__ __launch_bounds__(256) void sha1_fused_kernel(BatchArgs A) {
     if (S > 1) load_stage(en.p + 128, A1);
     uint32_t s = 0;
     for (; s + 1 < S; s += 2) {
-        fused_stage(s, S, en, A0, h);
-        fused_stage(s + 1, S, en, A1, h);
+        fused_stage<RV>(s, S, en, A0, h);
+        fused_stage<RV>(s + 1, S, en, A1, h);
     }
-    if (s < S) fused_stage(s, S, en, A0, h);
+    if (s < S) fused_stage<RV>(s, S, en, A0, h);
     if (valid) {
         lane_blocks(A, en, 2u * S, h);
         emit(A, en.id, h);
@@ -676,7 +680,19 @@ hipError_t launch_lane(const BatchArgs& A, hipStream_t st) {
 
 hipError_t launch_fused(const BatchArgs& A, hipStream_t st) {
     if (A.n == 0) return hipSuccess;
-    hipLaunchKernelGGL(sha1_fused_kernel, dim3((A.n + 255u) / 256u), dim3(256), 0, st, A);
+#ifdef SHA1CHUNK_AB_VARIANTS
+    if (const char* e = getenv("SHA1CHUNK_FUSED_VARIANT")) {
+        const int rv = atoi(e);
+        if (rv == 1)
+            hipLaunchKernelGGL(sha1_fused_kernel<1>, dim3((A.n + 255u) / 256u), dim3(256), 0, st, A);
+        else if (rv == 2)
+            hipLaunchKernelGGL(sha1_fused_kernel<2>, dim3((A.n + 255u) / 256u), dim3(256), 0, st, A);
+        else
+            return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
+#endif
+    hipLaunchKernelGGL(sha1_fused_kernel<0>, dim3((A.n + 255u) / 256u), dim3(256), 0, st, A);
     return hipGetLastError();
 }
 

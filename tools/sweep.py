@@ -53,11 +53,15 @@ def main():
                 if k.startswith("split") and k[5:].isdigit():  # split<U>: force the unit size
                     os.environ["SHA1CHUNK_SPLIT_UNIT"] = k[5:]
                     name = "split"
+                if k.startswith("fused") and k[5:].isdigit():  # fused<RV>: round-sum form (A/B lib)
+                    os.environ["SHA1CHUNK_FUSED_VARIANT"] = k[5:]
+                    name = "fused"
                 e0.record()
                 pkg.hash_uniform_device(buf, L, n, dig, kernel=name)
                 e1.record()
                 torch.cuda.synchronize()
                 os.environ.pop("SHA1CHUNK_SPLIT_UNIT", None)
+                os.environ.pop("SHA1CHUNK_FUSED_VARIANT", None)
                 times[k].append(e0.elapsed_time(e1))
                 d = dig.cpu().numpy()
                 if ref is None:
