@@ -20,6 +20,9 @@ struct BatchArgs {
     const uint32_t* init_state;  // 5 words per message instead of the IV
     uint64_t prefix_bytes;       // bytes already hashed before this call
     uint32_t* out_state;         // non-null: no padding, write raw state
+    // Mixed-batch kernel only: its device-side plan {mode, H, F}
+    // (plan_mixed_kernel, sha1_kernels.hip).
+    const uint32_t* plan;
 };
 
 hipError_t launch_lane(const BatchArgs& A, hipStream_t st);
@@ -31,13 +34,24 @@ hipError_t launch_fused(const BatchArgs& A, hipStream_t st);
 // flags (2, 3, 8-10, 12, 10*U+V, 500+V, 569, 577, 578).
 bool split_unit_built(int unit_blocks);
 hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st);
+// Sorted ragged batch of more groups than CUs (A.order set, sorted_len =
+// the lengths in that order): a device-side plan splits the groups between
+// the one-group split shape (longest first) and the fused kernel, or runs
+// them all in the 8-wave split shape (sha1_kernels.hip, mixed).  `plan`:
+// 3 device words; forced (or null): {mode, H, F} instead of the planner's.
+uint32_t mixed_grid(uint32_t groups, int cus, uint32_t* hcap);
+hipError_t launch_mixed(const BatchArgs& A, const uint32_t* sorted_len, uint32_t* plan, int cus,
+                        const int* forced, hipStream_t st);
 hipError_t launch_synth(uint8_t* dst, const uint64_t* off, const uint32_t* lens, uint32_t ulen,
                         uint64_t first, uint64_t count, uint64_t seed, hipStream_t st);
 hipError_t launch_compare(const uint8_t* dig, const uint8_t* exp, uint32_t n, uint8_t* mismatch,
                           hipStream_t st);
 
 // Longest-first order of a ragged batch (sha1_sort.hip): *d_order receives n
-// indices sorted by d_len descending; release *scratch with hipFreeAsync on
-// the same stream after the consuming kernel has been enqueued.
+// indices sorted by d_len descending, *d_sorted_len the lengths in that
+// order and *d_plan 16 spare bytes of the same allocation (for the mixed
+// kernel's plan); release *scratch with hipFreeAsync on the same stream
+// after the consuming kernel has been enqueued.
 hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t** d_order,
-                               void** scratch, hipStream_t st);
+                               const uint32_t** d_sorted_len, uint32_t** d_plan, void** scratch,
+                               hipStream_t st);

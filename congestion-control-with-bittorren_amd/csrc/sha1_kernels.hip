@@ -39,6 +39,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "sha1_device.hpp"
 #include "sha1_kernels.h"
 
@@ -442,9 +444,12 @@ struct ConsumeUnits {
 // half as long as the consumer's rounds, so the W+K hand-off, whose
 // VOP2-add consumer issues at the 4-cycle floor, is no longer producer-bound
 // (tools/consumer_probe, tools/replay_probe).
-template <int U, int PAIRS, int V = kSplitV<U>, int NPROD = 1>
-__global__ __launch_bounds__((kSplitThreads<PAIRS, V, NPROD>)) void sha1_split_kernel(
-    BatchArgs A) {
+// The body of one split workgroup `wg` (groups wg*PAIRS ..) over the LDS
+// array `lds` (PAIRS * 2 * U * kWBlockBytes bytes): sha1_split_kernel runs
+// it on blockIdx.x, the mixed-batch kernel on the workgroups its plan gives
+// to this shape.
+template <int U, int PAIRS, int V, int NPROD>
+__device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uint32_t wg) {
     constexpr bool WK = (V & kVWK) != 0;
     static_assert(PAIRS * 2 * U * kWBlockBytes <= 160 * 1024, "LDS");
     // Two producers for 2-block units (each owning one block per unit) were
@@ -453,7 +458,6 @@ __global__ __launch_bounds__((kSplitThreads<PAIRS, V, NPROD>)) void sha1_split_k
     static_assert(NPROD == 1 || (PAIRS == 1 && U == 2 * NPROD) ||
                       (PAIRS == 2 && U == NPROD && (V & kVLayout8) != 0),
                   "two producers: one stage (U = 4) or one block (U = 2, 8-wave layout) each per unit");
-    __shared__ __attribute__((aligned(16))) uint8_t lds[PAIRS * 2 * U * kWBlockBytes];
     int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     if constexpr ((V & kVSkipWave2) != 0) {
         static_assert(NPROD == 2 && PAIRS == 1, "skip-wave layout is for two producers");
@@ -474,7 +478,7 @@ __global__ __launch_bounds__((kSplitThreads<PAIRS, V, NPROD>)) void sha1_split_k
     }
     const int lane = threadIdx.x & 63;
     uint8_t* ring = lds + pair * (2 * U * kWBlockBytes);
-    const uint32_t group = blockIdx.x * PAIRS + (uint32_t)pair;
+    const uint32_t group = wg * PAIRS + (uint32_t)pair;
     const uint32_t e = group * 64u + (uint32_t)lane;
     const bool valid = e < A.n;
     Entry en = fetch_entry(A, valid ? e : min(group * 64u, A.n - 1u));
@@ -582,6 +586,13 @@ __global__ __launch_bounds__((kSplitThreads<PAIRS, V, NPROD>)) void sha1_split_k
     }
 }
 
+template <int U, int PAIRS, int V = kSplitV<U>, int NPROD = 1>
+__global__ __launch_bounds__((kSplitThreads<PAIRS, V, NPROD>)) void sha1_split_kernel(
+    BatchArgs A) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[PAIRS * 2 * U * kWBlockBytes];
+    split_body<U, PAIRS, V, NPROD>(A, lds, blockIdx.x);
+}
+
 // --------------------------------------------------------------- fused ----
 // One wave, 64 chunks, schedule and rounds in registers (~630 VALU per
 // block).  Best once there are enough chunks for two or more waves per SIMD:
@@ -604,9 +615,9 @@ __device__ __forceinline__ void fused_stage(uint32_t s, uint32_t S, const Entry&
 
 // RV: round-sum form (sha1_device.hpp round_step); the product uses 0, the
 // A/B library also builds 1 and 2 (SHA1CHUNK_FUSED_VARIANT).
-template <int RV = 0>
-__global__ __launch_bounds__(256) void sha1_fused_kernel(BatchArgs A) {
-    const uint32_t e = blockIdx.x * 256u + threadIdx.x;
+// The body of one fused wave: message e's lane (group e / 64).
+template <int RV>
+__device__ __forceinline__ void fused_body(const BatchArgs& A, uint32_t e) {
     const uint32_t group = e / 64u;
     const bool valid = e < A.n;
     Entry en = fetch_entry(A, valid ? e : min(group * 64u, A.n - 1u));
@@ -630,6 +641,237 @@ __global__ __launch_bounds__(256) void sha1_fused_kernel(BatchArgs A) {
     if (valid) {
         lane_blocks(A, en, 2u * S, h);
         emit(A, en.id, h);
+    }
+}
+
+template <int RV = 0>
+__global__ __launch_bounds__(256) void sha1_fused_kernel(BatchArgs A) {
+    fused_body<RV>(A, blockIdx.x * 256u + threadIdx.x);
+}
+
+// --------------------------------------------------------------- mixed ----
+// Ragged batches with more groups of 64 than CUs, sorted longest-first
+// (BASELINE config 5's shape beyond 16384 chunks).  A batch of mixed lengths
+// ends with its longest chunks' serial chains, so the kernel that has the
+// most throughput per CU (fused) is not the one to run them on: at several
+// waves per SIMD a fused wave's chain crawls (2.4 us per block at 2 waves
+// per SIMD against 0.74 us in the one-group split shape), and a batch of
+// log-uniform 4 KiB .. 1 MiB chunks ran 2.5x longer fused than split
+// (tools/mixed_bench.py, profiles/mixed_r02.json).  A device-side plan
+// (plan_mixed_kernel, from the sorted lengths, no host round trip) splits
+// the batch between the shapes; every workgroup of this kernel reserves the
+// whole 160 KiB of LDS, so exactly one is resident per CU:
+//   mode 0: workgroups 0 .. H-1 hash groups 0 .. H-1 (the longest) one per
+//           CU in the one-group split shape (4-block units, two producers,
+//           the consumer alone on its SIMD); workgroup H + j hashes groups
+//           H + j*F .. H + j*F + F-1 fused, one group per wave (F = 4: one
+//           wave per SIMD, chain 1.28 us per block; F = 8: two).
+//   mode 1: workgroup w hashes groups 2w, 2w+1 in the 8-wave two-pair split
+//           shape (AUTO's shape for C < groups <= 2C on a uniform batch).
+// Blocks in dispatch order: the longest groups start first, and the
+// hardware dispatcher hands the next workgroup to whichever CU frees up
+// (longest-processing-time order).  The grid is one workgroup per group
+// (the all-split plan); workgroups past a plan's count exit at once.
+//
+// Memory locality decides as much as the model below: every lane streams
+// its own chunk, so the chip keeps one address translation per chunk in
+// flight, and when a group's 64 chunks lie far apart (a sorted batch whose
+// chunks arrived in random length order) the fused tail's many resident
+// chunks thrash them: 65536 x 512 KiB with permuted offsets hash in 28.9 ms
+// fused against 10.6 ms in place, and the config-5 law at 65536 chunks in
+// arrival order runs its all-fused plan at 1.98 us per block against 1.28
+// for the same lengths laid out longest-first (profiles/mixed_r02.json).
+// The planner therefore sends a scattered batch (most of its work in
+// groups whose chunks span more than 4x their bytes + 4 MiB of address
+// space) to the one-group split shape whole: a quarter of the resident
+// chunks per CU of the fused tail, and the shortest chains.
+constexpr int kSplit8V = kVWK | kVUnmask | kVLayout8 | kVCross;
+constexpr int kMixedThreads = 512;
+
+__global__ __launch_bounds__(kMixedThreads) void sha1_mixed_kernel(BatchArgs A) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[160 * 1024];
+    const uint32_t mode = A.plan[0], H = A.plan[1], F = A.plan[2];
+    const uint32_t wg = blockIdx.x;
+    const uint32_t groups = (A.n + 63u) / 64u;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if (mode == 1) {
+        if (2u * wg >= groups) return;
+        split_body<2, 2, kSplit8V, 2>(A, lds, wg);
+        return;
+    }
+    if (wg < H) {
+        if (wave >= 4) return;  // the one-group shape is waves 0-3 (wave 2 empty)
+        split_body<4, 1, kSplitV<4>, kSplitNProd<4>>(A, lds, wg);
+        return;
+    }
+    const uint32_t g = H + (wg - H) * F + wave;
+    if (wave >= F || g >= groups) return;
+    fused_body<0>(A, g * 64u + (threadIdx.x & 63u));
+}
+
+// Makespan model of a sorted ragged batch, microseconds per 64-byte block of
+// a group of 64 chunks, measured on MI355X:
+//   chain: time of one group's block when it runs in that shape
+//   cu:    CU-time per group-block (the CU's throughput in that shape)
+// one-group split: config 2, 6.08 ms / 8193 blocks, one group per CU.
+// fused F = 4 (one wave per SIMD): 65536 x 512 KiB, 10.5 ms; F = 8 (two):
+// 131072 x 512 KiB, 19.9 ms.  8-wave split: 32768 x 512 KiB, 6.55 ms.
+constexpr double kChainSplit4 = 0.742, kCuSplit4 = 0.742;
+constexpr double kChainFused4 = 1.28, kCuFused4 = 0.320;
+constexpr double kChainFused8 = 2.43, kCuFused8 = 0.304;
+constexpr double kChainSplit8 = 0.80, kCuSplit8 = 0.40;
+
+__device__ __forceinline__ uint32_t group_blocks(const uint32_t* sorted_len, uint32_t g) {
+    return total_blocks(sorted_len[64ull * g]);  // a group's first lane is its longest
+}
+
+// The workgroups of a plan are jobs that the dispatcher starts in index
+// order on whichever CU frees first.  Job i of mode 0 (H split groups, then
+// fused workgroups of F groups) and of mode 1 (pairs): its duration.
+__device__ __forceinline__ double job_time(const uint32_t* sorted_len, uint32_t mode, uint32_t H,
+                                           uint32_t F, uint32_t i) {
+    if (mode == 1) return group_blocks(sorted_len, 2u * i) * kChainSplit8;
+    if (i < H) return group_blocks(sorted_len, i) * kChainSplit4;
+    return group_blocks(sorted_len, H + (i - H) * F) * (F == 4 ? kChainFused4 : kChainFused8);
+}
+
+// Estimated makespan of a plan: the largest of
+//   W / C                         total CU-time over C CUs (work bound)
+//   p_0, p_H                      the longest split job, the longest fused job
+//   (k + 1) p_{kC}, k >= 1        jobs 0 .. kC on C CUs: some CU runs k + 1
+//                                 of them back to back (rounds bound; exact
+//                                 for equal lengths)
+// where W = cu_split4 * P_H + cu_fusedF * (P_G - P_H) in mode 0 and
+// cu_split8 * P_G in mode 1 (P_H: blocks of groups 0 .. H-1).
+__device__ double makespan(const uint32_t* sorted_len, uint32_t G, uint32_t C, uint32_t mode, uint32_t H,
+                           uint32_t F, uint64_t PH, uint64_t PG) {
+    double W;
+    uint32_t J;
+    if (mode == 1) {
+        W = kCuSplit8 * (double)PG;
+        J = (G + 1u) / 2u;
+    } else {
+        W = kCuSplit4 * (double)PH + (F == 4 ? kCuFused4 : kCuFused8) * (double)(PG - PH);
+        J = H + (G - H + F - 1u) / F;
+    }
+    double m = fmax(W / C, job_time(sorted_len, mode, H, F, 0));
+    if (mode == 0 && H > 0 && H < G) m = fmax(m, job_time(sorted_len, mode, H, F, H));
+    for (uint32_t k = 1; (uint64_t)k * C < J; ++k)
+        m = fmax(m, (k + 1) * job_time(sorted_len, mode, H, F, k * C));
+    return m;
+}
+
+// One workgroup.  A scattered batch (see the kernel's comment) gets the
+// all-split plan {0, G, 4}; otherwise every plan is evaluated -- mode 0 with
+// H in [0, hcap] or H = G and F in {4, 8}, and mode 1 -- and the smallest
+// estimate wins (ties: mode 0, smaller H).  forced: write {fmode, fh, ff}
+// as given (tests, A/B).
+constexpr int kPlanThreads = 1024;
+constexpr uint32_t kPlanMaxH = 4096;  // largest split head the model search considers
+
+// Whether group g's chunks lie close together: their address span (first
+// byte to last) against their bytes.
+__device__ __forceinline__ bool group_scattered(const BatchArgs& A, uint32_t g) {
+    uint64_t lo = ~0ull, hi = 0, bytes = 0;
+    const uint32_t e1 = min(A.n, 64u * g + 64u);
+    for (uint32_t e = 64u * g; e < e1; ++e) {
+        const uint32_t id = A.order[e];
+        const uint64_t o = A.off[id], l = A.len[id];
+        lo = min(lo, o);
+        hi = max(hi, o + l);
+        bytes += l;
+    }
+    return hi > lo && hi - lo > 4ull * bytes + (4ull << 20);
+}
+
+__global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, const uint32_t* sorted_len,
+                                                                  uint32_t cus, uint32_t hcap, int forced,
+                                                                  uint32_t fmode, uint32_t fh, uint32_t ff,
+                                                                  uint32_t* plan) {
+    const uint32_t n = A.n;
+    const uint32_t t = threadIdx.x;
+    if (forced) {
+        if (t == 0) {
+            plan[0] = fmode;
+            plan[1] = fh;
+            plan[2] = ff;
+        }
+        return;
+    }
+    __shared__ uint64_t scan[kPlanThreads];
+    __shared__ double best_m[kPlanThreads];
+    __shared__ uint32_t best_h[kPlanThreads], best_f[kPlanThreads];
+    __shared__ uint64_t prefix[kPlanMaxH + 1];
+    const uint32_t G = (n + 63u) / 64u;
+    const uint32_t per = (G + kPlanThreads - 1) / kPlanThreads;
+    const uint32_t g0 = min(G, t * per), g1 = min(G, g0 + per);
+    uint64_t local = 0, local_far = 0;
+    for (uint32_t g = g0; g < g1; ++g) {
+        const uint32_t b = group_blocks(sorted_len, g);
+        local += b;
+        if (group_scattered(A, g)) local_far += b;
+    }
+    __shared__ uint64_t far_sum;
+    if (t == 0) far_sum = 0;
+    __syncthreads();
+    if (local_far) atomicAdd(reinterpret_cast<unsigned long long*>(&far_sum), (unsigned long long)local_far);
+    scan[t] = local;
+    __syncthreads();
+    for (uint32_t off = 1; off < kPlanThreads; off <<= 1) {
+        const uint64_t v = t >= off ? scan[t - off] : 0ull;
+        __syncthreads();
+        scan[t] += v;
+        __syncthreads();
+    }
+    const uint64_t PG = scan[kPlanThreads - 1];
+    if (2 * far_sum > PG) {  // scattered: every group in the one-group split shape
+        if (t == 0) {
+            plan[0] = 0;
+            plan[1] = G;
+            plan[2] = 4;
+        }
+        return;
+    }
+    // P_H for every candidate H <= hcap, then each thread takes H = t, t + 1024, ..
+    uint64_t P = scan[t] - local;  // P_{g0}
+    for (uint32_t g = g0; g <= g1 && g <= hcap; ++g) {
+        prefix[g] = P;
+        if (g < g1) P += group_blocks(sorted_len, g);
+    }
+    __syncthreads();
+    double bm = 1e300;
+    uint32_t bh = 0, bf = 4;
+    for (uint32_t H = t; H <= hcap; H += kPlanThreads) {
+        for (uint32_t F = 4; F <= (H < G ? 8u : 4u); F += 4) {  // H = G: every group split
+            const double m = makespan(sorted_len, G, cus, 0, H, F, prefix[H], PG);
+            if (m < bm) { bm = m; bh = H; bf = F; }
+        }
+    }
+    if (t == 0 && G > hcap) {  // H = G beyond the searched head sizes
+        const double m = makespan(sorted_len, G, cus, 0, G, 4, PG, PG);
+        if (m < bm) { bm = m; bh = G; bf = 4; }
+    }
+    best_m[t] = bm;
+    best_h[t] = bh;
+    best_f[t] = bf;
+    __syncthreads();
+    for (uint32_t s = kPlanThreads / 2; s > 0; s >>= 1) {
+        if (t < s) {
+            const double mo = best_m[t + s];
+            const uint32_t ho = best_h[t + s];
+            if (mo < best_m[t] || (mo == best_m[t] && ho < best_h[t])) {
+                best_m[t] = mo;
+                best_h[t] = ho;
+                best_f[t] = best_f[t + s];
+            }
+        }
+        __syncthreads();
+    }
+    if (t == 0) {
+        const bool split8 = makespan(sorted_len, G, cus, 1, 0, 0, 0, PG) < best_m[0];
+        plan[0] = split8 ? 1u : 0u;
+        plan[1] = split8 ? 0u : best_h[0];
+        plan[2] = split8 ? 0u : best_f[0];
     }
 }
 
@@ -721,8 +963,8 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
         break;
     case 11:  // <= 2 groups per CU: 2 pairs x (consumer + 2 producers), 2-block
               // units, 8-wave layout, producer SIMDs crossed between the pairs
-        hipLaunchKernelGGL((sha1_split_kernel<2, 2, kVWK | kVUnmask | kVLayout8 | kVCross, 2>),
-                           dim3((groups + 1) / 2), dim3(512), 0, st, A);
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, kSplit8V, 2>), dim3((groups + 1) / 2), dim3(512), 0,
+                           st, A);
         break;
 #ifdef SHA1CHUNK_AB_VARIANTS
     // The shapes and variants of the split-kernel study (profiles/sweep_r01.json,
@@ -787,6 +1029,29 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
 #endif
     default: return hipErrorInvalidValue;
     }
+    return hipGetLastError();
+}
+
+uint32_t mixed_grid(uint32_t groups, int cus, uint32_t* hcap) {
+    *hcap = std::min<uint32_t>(std::min<uint32_t>(groups, 4u * (uint32_t)cus), kPlanMaxH);
+    // the largest workgroup count of any plan: every group split (H = G)
+    return groups;
+}
+
+hipError_t launch_mixed(const BatchArgs& A, const uint32_t* sorted_len, uint32_t* plan, int cus,
+                        const int* forced, hipStream_t st) {
+    if (A.n == 0) return hipSuccess;
+    const uint32_t groups = (A.n + 63u) / 64u;
+    uint32_t hcap;
+    const uint32_t grid = mixed_grid(groups, cus, &hcap);
+    hipLaunchKernelGGL(plan_mixed_kernel, dim3(1), dim3(kPlanThreads), 0, st, A, sorted_len,
+                       (uint32_t)cus, hcap, forced ? 1 : 0, forced ? (uint32_t)forced[0] : 0u,
+                       forced ? (uint32_t)forced[1] : 0u, forced ? (uint32_t)forced[2] : 0u, plan);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    BatchArgs B = A;
+    B.plan = plan;
+    hipLaunchKernelGGL(sha1_mixed_kernel, dim3(grid), dim3(kMixedThreads), 0, st, B);
     return hipGetLastError();
 }
 

@@ -306,6 +306,50 @@ int launch_checked(int kernel, const BatchArgs& A, hipStream_t st, int cus = 256
     return SHA1CHUNK_OK;
 }
 
+// Mixed kernel for sorted ragged batches of more groups than CUs, unless an
+// A/B hook forces a kernel behind AUTO (SHA1CHUNK_FORCE_KERNEL) or
+// SHA1CHUNK_MIXED=0 turns it off (then AUTO's uniform-batch rule applies).
+bool use_mixed() {
+    if (getenv("SHA1CHUNK_FORCE_KERNEL")) return false;
+    const char* e = getenv("SHA1CHUNK_MIXED");
+    return !(e && !strcmp(e, "0"));
+}
+
+// SHA1CHUNK_MIXED_PLAN="mode,H,F" replaces the device-side plan (tests and
+// A/B runs): mode 0 with 0 <= H <= min(groups, 4 CUs) and F in {4, 8}, or
+// mode 1.  SHA1CHUNK_MIXED_DEBUG=1 prints the plan used (synchronises the
+// stream: diagnostics only).
+int launch_mixed_checked(const BatchArgs& A, const uint32_t* sorted_len, uint32_t* plan, int cus,
+                         hipStream_t st) {
+    if (A.n > 0 && (reinterpret_cast<uintptr_t>(A.dig) & 3u))
+        return fail(SHA1CHUNK_EALIGN, "digest buffer must be 4-byte aligned");
+    int forced[3] = {0, 0, 0};
+    bool force = false;
+    if (const char* e = getenv("SHA1CHUNK_MIXED_PLAN")) {
+        uint32_t hcap;
+        const uint32_t groups = (A.n + 63u) / 64u, grid = mixed_grid(groups, cus, &hcap);
+        if (sscanf(e, "%d,%d,%d", &forced[0], &forced[1], &forced[2]) != 3 || forced[0] < 0 ||
+            forced[0] > 1 ||
+            (forced[0] == 0 && (forced[1] < 0 || ((uint32_t)forced[1] > hcap && (uint32_t)forced[1] != groups) ||
+                                (forced[2] != 4 && forced[2] != 8))))
+            return fail(SHA1CHUNK_EINVAL,
+                        "SHA1CHUNK_MIXED_PLAN=%s: want 0,H,F (0 <= H <= %u or H = %u, F 4|8) or 1,0,0", e,
+                        hcap, groups);
+        (void)grid;
+        force = true;
+    }
+    hipError_t e = launch_mixed(A, sorted_len, plan, cus, force ? forced : nullptr, st);
+    if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "mixed kernel launch: %s", hipGetErrorString(e));
+    if (const char* d = getenv("SHA1CHUNK_MIXED_DEBUG"); d && atoi(d)) {
+        uint32_t p[3];
+        HIP_TRY(hipMemcpyAsync(p, plan, sizeof p, hipMemcpyDeviceToHost, st));
+        HIP_TRY(hipStreamSynchronize(st));
+        fprintf(stderr, "sha1chunk mixed plan: n=%u groups=%u cus=%d mode=%u H=%u F=%u\n", A.n,
+                (A.n + 63u) / 64u, cus, p[0], p[1], p[2]);
+    }
+    return SHA1CHUNK_OK;
+}
+
 // ------------------------------------------------------------ host batch --
 // Host batches go through two pipeline slots (own stream each), so the H2D
 // copy of slot b+1 overlaps the kernel of slot b.  A slot's bytes come
@@ -574,11 +618,20 @@ int sha1chunk_hash_device_async(const void* d_base, const uint64_t* d_offsets,
     A.n = static_cast<uint32_t>(n);
     A.dig = d_digests;
     hipStream_t st = static_cast<hipStream_t>(stream);
-    // AUTO on a ragged batch: hash longest-first (sha1_sort.hip).
+    // AUTO on a ragged batch: hash longest-first (sha1_sort.hip); with more
+    // groups of 64 than CUs, through the mixed kernel and its device-side
+    // plan (sha1_kernels.hip, mixed).
     void* scratch = nullptr;
     if (kernel == SHA1CHUNK_KERNEL_AUTO && n > 64) {
-        hipError_t e = sort_by_length_desc(d_lengths, A.n, &A.order, &scratch, st);
+        const uint32_t* sorted_len = nullptr;
+        uint32_t* plan = nullptr;
+        hipError_t e = sort_by_length_desc(d_lengths, A.n, &A.order, &sorted_len, &plan, &scratch, st);
         if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "length sort: %s", hipGetErrorString(e));
+        if ((n + 63) / 64 > size_t(D->cus) && use_mixed()) {
+            rc = launch_mixed_checked(A, sorted_len, plan, D->cus, st);
+            (void)hipFreeAsync(scratch, st);
+            return rc;
+        }
     }
     rc = launch_checked(choose_kernel(kernel, n, D->cus), A, st, D->cus);
     if (scratch) (void)hipFreeAsync(scratch, st);

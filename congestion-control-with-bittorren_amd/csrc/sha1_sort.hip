@@ -25,8 +25,11 @@ inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 }  // namespace
 
 hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t** d_order,
-                               void** scratch, hipStream_t st) {
+                               const uint32_t** d_sorted_len, uint32_t** d_plan, void** scratch,
+                               hipStream_t st) {
     *d_order = nullptr;
+    *d_sorted_len = nullptr;
+    *d_plan = nullptr;
     *scratch = nullptr;
     size_t temp_bytes = 0;
     hipError_t e = hipcub::DeviceRadixSort::SortPairsDescending(
@@ -35,13 +38,14 @@ hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t
     if (e != hipSuccess) return e;
     const size_t arr = align256(size_t(n) * sizeof(uint32_t));
     void* base = nullptr;
-    e = hipMallocAsync(&base, 3 * arr + align256(temp_bytes), st);
+    e = hipMallocAsync(&base, 3 * arr + 256 + align256(temp_bytes), st);
     if (e != hipSuccess) return e;
     uint8_t* b = static_cast<uint8_t*>(base);
     uint32_t* keys_out = reinterpret_cast<uint32_t*>(b);
     uint32_t* vals_in = reinterpret_cast<uint32_t*>(b + arr);
     uint32_t* vals_out = reinterpret_cast<uint32_t*>(b + 2 * arr);
-    void* temp = b + 3 * arr;
+    uint32_t* plan = reinterpret_cast<uint32_t*>(b + 3 * arr);
+    void* temp = b + 3 * arr + 256;
     hipLaunchKernelGGL(iota_kernel, dim3((n + 255) / 256), dim3(256), 0, st, vals_in, n);
     if ((e = hipGetLastError()) != hipSuccess) {
         (void)hipFreeAsync(base, st);
@@ -54,6 +58,8 @@ hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t
         return e;
     }
     *d_order = vals_out;
+    *d_sorted_len = keys_out;
+    *d_plan = plan;
     *scratch = base;
     return hipSuccess;
 }

@@ -1,0 +1,271 @@
+"""The mixed-batch kernel (sha1_kernels.hip, `mixed`): sorted ragged device
+batches with more groups of 64 chunks than CUs, split between the one-group
+split shape (the longest groups) and the fused kernel, or run in the 8-wave
+split shape, by a device-side plan (plan_mixed_kernel).  Every plan shape is
+forced with SHA1CHUNK_MIXED_PLAN and checked bit-exact against the oracle;
+the planner's choice is checked against its restatement here; the config-5
+length law at 4x its size is checked against the plain kernels."""
+import hashlib
+import math
+import os
+import re
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+# plan_mixed_kernel's model (us per block of a group of 64 chunks)
+CHAIN = {"split4": 0.742, "fused4": 1.28, "fused8": 2.43, "split8": 0.80}
+CU = {"split4": 0.742, "fused4": 0.320, "fused8": 0.304, "split8": 0.40}
+PLAN_MAX_H = 4096
+
+
+@pytest.fixture(scope="module")
+def dev(pkg):
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a device"
+    torch.cuda.set_device(0)
+    pkg.set_device(0)
+    return torch
+
+
+@pytest.fixture(scope="module")
+def cus(dev):
+    return dev.cuda.get_device_properties(0).multi_processor_count
+
+
+def total_blocks(ln):
+    ln = np.asarray(ln, np.int64)
+    return (ln >> 6) + np.where((ln & 63) < 56, 1, 2)
+
+
+def grid_of(G, C):
+    return min(G, 4 * C, PLAN_MAX_H), G
+
+
+def model_makespan(B, C, mode, H, F, P):
+    """plan_mixed_kernel's `makespan`, restated."""
+    G = len(B)
+    if mode == 1:
+        W, J = CU["split8"] * P[G], (G + 1) // 2
+        job = lambda i: B[2 * i] * CHAIN["split8"]
+    else:
+        fk = f"fused{F}"
+        W = CU["split4"] * P[H] + CU[fk] * (P[G] - P[H])
+        J = H + (G - H + F - 1) // F
+        job = lambda i: B[i] * CHAIN["split4"] if i < H else B[H + (i - H) * F] * CHAIN[fk]
+    m = max(W / C, job(0))
+    if mode == 0 and 0 < H < G:
+        m = max(m, job(H))
+    k = 1
+    while k * C < J:
+        m = max(m, (k + 1) * job(k * C))
+        k += 1
+    return m
+
+
+def scattered_work(order, off, lens, B):
+    """plan_mixed_kernel's locality test, restated: the share of the work in
+    groups whose chunks span more than 4x their bytes + 4 MiB."""
+    far = 0
+    for g, b in enumerate(B):
+        ids = order[64 * g:64 * g + 64]
+        o, ln = off[ids].astype(np.int64), lens[ids].astype(np.int64)
+        span = int((o + ln).max() - o.min())
+        if span > 4 * int(ln.sum()) + (4 << 20):
+            far += b
+    return far
+
+
+def model_plan(lengths, C, off=None):
+    """plan_mixed_kernel's search, restated: (estimate, mode, H, F)."""
+    lengths = np.asarray(lengths, np.int64)
+    order = np.argsort(-lengths, kind="stable")  # the device's stable radix sort
+    srt = lengths[order]
+    B = [int(b) for b in total_blocks(srt[::64])]
+    G = len(B)
+    P = [0]
+    for b in B:
+        P.append(P[-1] + b)
+    if off is not None and 2 * scattered_work(order, off, lengths, B) > P[G]:
+        return (model_makespan(B, C, 0, G, 4, P), 0, G, 4), (B, P)
+    hcap, grid = grid_of(G, C)
+    best = None
+    for H in list(range(hcap + 1)) + ([G] if G > hcap else []):
+        for F in ((4, 8) if H < G else (4,)):
+            m = model_makespan(B, C, 0, H, F, P)
+            if best is None or m < best[0]:
+                best = (m, 0, H, F)
+    m = model_makespan(B, C, 1, 0, 0, P)
+    if m < best[0]:
+        best = (m, 1, 0, 0)
+    return best, (B, P)
+
+
+def ragged(rng, n, long_n, long_lo, long_hi, short_hi, aligned=True):
+    lens = rng.integers(0, short_hi, n).astype(np.uint32)
+    lens[:long_n] = rng.integers(long_lo, long_hi, long_n)
+    lens[rng.choice(n, 40, replace=False)] = 0
+    lens[rng.choice(n, 40, replace=False)] = 55
+    lens[rng.choice(n, 40, replace=False)] = 56
+    rng.shuffle(lens)
+    step = ((lens.astype(np.uint64) + 63) // 64 * 64 if aligned
+            else lens.astype(np.uint64) + rng.integers(1, 40, n).astype(np.uint64))
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(step)[: n - 1]
+    host = rng.integers(0, 256, int(off[-1] + lens[-1]) + 64, dtype=np.uint8)
+    return host, off, lens
+
+
+def run(pkg, torch, host, off, lens, env, monkeypatch, kernel="auto"):
+    for k in ("SHA1CHUNK_MIXED_PLAN", "SHA1CHUNK_MIXED_DEBUG", "SHA1CHUNK_MIXED"):
+        monkeypatch.delenv(k, raising=False)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    n = lens.size
+    d_dig = torch.zeros((n, 20), dtype=torch.uint8, device="cuda")
+    pkg.hash_device(torch.from_numpy(host).cuda(), torch.from_numpy(off.astype(np.int64)).cuda(),
+                    torch.from_numpy(lens.astype(np.int32)).cuda(), d_dig, kernel=kernel)
+    torch.cuda.synchronize()
+    return d_dig.cpu().numpy()
+
+
+def _check(got, want, what):
+    bad = np.nonzero((got != want).any(axis=1))[0]
+    assert bad.size == 0, f"{what}: {bad.size} bad digests, first {bad[:8]}"
+
+
+@pytest.mark.parametrize("aligned", [True, False])
+def test_mixed_every_plan_shape(pkg, dev, oracle, cus, monkeypatch, aligned):
+    """~1.2 x CUs groups: split head sizes 0, 1, odd, all; fused tails of 4
+    and 8 groups per workgroup (last one partial); the 8-wave mode; the
+    planner's own choice.  Misaligned starts take every kernel's per-lane
+    load fallback."""
+    torch = dev
+    rng = np.random.default_rng(77 + aligned)
+    G = cus + cus // 5 + 1
+    n = 64 * G - 23  # a partial last group
+    host, off, lens = ragged(rng, n, 2500, 60000, 140000, 9000, aligned)
+    want = oracle.hash_batch(host, off, lens)
+    hcap, _ = grid_of(G, cus)
+    plans = ["0,0,4", "0,0,8", "0,1,4", "0,37,8", f"0,{hcap},4", f"0,{G // 2},4", "1,0,0", None]
+    for p in plans:
+        got = run(pkg, torch, host, off, lens, {"SHA1CHUNK_MIXED_PLAN": p} if p else {}, monkeypatch)
+        _check(got, want, f"plan {p or 'device'} aligned={aligned}")
+
+
+def test_mixed_head_capped_below_groups(pkg, dev, oracle, cus, monkeypatch):
+    """More than 4 x CUs groups: the model's split heads stop at hcap <
+    groups, the all-split plan (H = G) is still allowed, and every plan's
+    workgroups must cover every group."""
+    torch = dev
+    rng = np.random.default_rng(5)
+    G = 4 * cus + 70
+    n = 64 * G - 5
+    host, off, lens = ragged(rng, n, 300, 20000, 40000, 1500)
+    want = oracle.hash_batch(host, off, lens)
+    hcap, grid = grid_of(G, cus)
+    assert hcap < G
+    plans = [f"0,{hcap},4", f"0,{hcap},8", "0,3,8", "0,0,4", f"0,{G},4", "1,0,0", None]
+    for p in plans:
+        got = run(pkg, torch, host, off, lens, {"SHA1CHUNK_MIXED_PLAN": p} if p else {}, monkeypatch)
+        _check(got, want, f"plan {p or 'device'} G={G}")
+
+
+def test_mixed_invalid_plan_fails_loudly(pkg, dev, cus, monkeypatch):
+    torch = dev
+    n = 64 * (cus + 3)
+    lens = np.full(n, 100, np.uint32)
+    off = np.arange(n, dtype=np.uint64) * 128
+    host = np.zeros(n * 128, np.uint8)
+    G = (n + 63) // 64
+    hcap, _ = grid_of(G, cus)
+    bad_h = hcap + 1 if hcap + 1 != G else G + 1
+    for p in (f"0,{bad_h},4", f"0,{G + 1},4", "0,5,3", "2,0,0", "junk"):
+        with pytest.raises(pkg.Sha1ChunkError, match="SHA1CHUNK_MIXED_PLAN"):
+            run(pkg, torch, host, off, lens, {"SHA1CHUNK_MIXED_PLAN": p}, monkeypatch)
+
+
+def _device_plan(capfd):
+    err = capfd.readouterr().err
+    m = re.findall(r"mixed plan: n=(\d+) groups=(\d+) cus=(\d+) mode=(\d+) H=(\d+) F=(\d+)", err)
+    assert m, err
+    return tuple(int(x) for x in m[-1][3:])
+
+
+@pytest.mark.parametrize("shape", ["uniform_64k_2.4C", "uniform_8k_4.3C", "mixed_log", "mixed_log_sorted",
+                                   "two_level", "two_level_sorted"])
+def test_mixed_planner_matches_model(pkg, dev, cus, monkeypatch, capfd, shape):
+    """The device planner's plan is the best plan of its model restated here
+    (up to ties), on uniform, log-uniform and two-level length mixes, laid
+    out in arrival order (a sorted batch's groups are scattered: all-split
+    plan) and longest-first (contiguous groups: the model's search)."""
+    torch = dev
+    rng = np.random.default_rng(9)
+    if shape == "uniform_64k_2.4C":
+        lens = np.full(int(64 * cus * 2.4), 65536, np.uint32)
+    elif shape == "uniform_8k_4.3C":
+        lens = np.full(int(64 * cus * 4.3), 8192, np.uint32)
+    elif shape.startswith("mixed_log"):
+        lens = (4096 * 2.0 ** rng.uniform(0, 8, 64 * cus * 3)).astype(np.uint32)
+    else:
+        lens = np.where(rng.uniform(size=64 * cus * 2) < 0.1, 1 << 20, 4096).astype(np.uint32)
+    if shape.endswith("_sorted"):
+        lens = np.sort(lens)[::-1].copy()
+    n = lens.size
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum((lens.astype(np.uint64) + 63) // 64 * 64)[: n - 1]
+    base = torch.zeros(int(off[-1] + lens[-1]) + 64, dtype=torch.uint8, device="cuda")
+    for k in ("SHA1CHUNK_MIXED_PLAN", "SHA1CHUNK_MIXED"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("SHA1CHUNK_MIXED_DEBUG", "1")
+    dig = torch.zeros((n, 20), dtype=torch.uint8, device="cuda")
+    pkg.hash_device(base, torch.from_numpy(off.astype(np.int64)).cuda(),
+                    torch.from_numpy(lens.astype(np.int32)).cuda(), dig)
+    torch.cuda.synchronize()
+    mode, H, F = _device_plan(capfd)
+    (best, bmode, bH, bF), (B, P) = model_plan(lens, cus, off)
+    if shape == "mixed_log":  # sorted groups of arrival-order chunks of distinct lengths: scattered
+        assert (bmode, bH, bF) == (0, len(B), 4), shape
+        assert (mode, H, F) == (0, len(B), 4), shape
+    else:
+        got = model_makespan(B, cus, mode, H, F, P)
+        assert got <= best * (1 + 1e-9), (shape, (mode, H, F), got, (bmode, bH, bF), best)
+    # every chunk of these batches holds zeros: one digest per distinct length
+    d = dig.cpu().numpy()
+    for L in rng.choice(np.unique(lens), 12):
+        i = int(np.nonzero(lens == L)[0][0])
+        assert d[i].tobytes() == hashlib.sha1(bytes(int(L))).digest()
+
+
+def test_mixed_config5_law_at_4x(pkg, dev, oracle, cus, monkeypatch):
+    """BASELINE config 5's length law (4 KiB .. 1 MiB, ragged tails) at 65536
+    chunks (12 GiB resident, 4 groups per CU): AUTO's mixed kernel against
+    the plain fused kernel in caller order, the first 16384 digests against
+    the reference golden vectors, and a sample against hashlib."""
+    torch = dev
+    n = 65536
+    lens = oracle.mixed_lengths(n)
+    off, total = pkg.sha1chunk.ragged_layout(lens)
+    d_base = torch.zeros(total + 128, dtype=torch.uint8, device="cuda")
+    d_off = torch.from_numpy(off.astype(np.int64)).cuda()
+    d_len = torch.from_numpy(lens.astype(np.int32)).cuda()
+    pkg.synth_fill_ragged_device(d_base, d_off, d_len, 0)
+    for k in ("SHA1CHUNK_MIXED_PLAN", "SHA1CHUNK_MIXED", "SHA1CHUNK_MIXED_DEBUG"):
+        monkeypatch.delenv(k, raising=False)
+    outs = {}
+    for kernel in ("auto", "fused"):
+        dig = torch.zeros((n, 20), dtype=torch.uint8, device="cuda")
+        pkg.hash_device(d_base, d_off, d_len, dig, kernel=kernel)
+        torch.cuda.synchronize()
+        outs[kernel] = dig.cpu().numpy()
+    _check(outs["auto"], outs["fused"], "mixed vs fused")
+    want = np.fromfile(os.path.join(os.path.dirname(__file__), "golden", "mixed_16384.bin"),
+                       np.uint8).reshape(-1, 20)
+    _check(outs["auto"][:16384], want, "first 16384 vs reference golden")
+    for i in np.unique(np.linspace(16384, n - 1, 12).astype(np.int64)):
+        o, L = int(off[i]), int(lens[i])
+        assert hashlib.sha1(d_base[o:o + L].cpu().numpy().tobytes()).digest() == outs["auto"][i].tobytes()
+    del d_base
+    torch.cuda.empty_cache()
