@@ -43,12 +43,17 @@ enum {
 #define SHA1CHUNK_ALL_DEVICES 2u /* HOST only: shard the chunk list over every
                                     visible device, one host thread per device */
 
-/* Kernel choice for the device entry points (AUTO picks by batch shape). */
+/* Kernel choice for the device entry points (AUTO picks by batch shape:
+ * the split kernel up to two groups of 64 chunks per CU, the fused kernel
+ * beyond; a ragged batch is hashed longest-first, and with more groups than
+ * CUs through the mixed kernel, whose device-side plan splits the groups
+ * between the one-group split shape and the fused kernel). */
 enum {
     SHA1CHUNK_KERNEL_AUTO = 0,
-    SHA1CHUNK_KERNEL_LANE = 1,  /* one lane per chunk, per-lane loads; any alignment */
-    SHA1CHUNK_KERNEL_FUSED = 2, /* one lane per chunk, LDS-staged coalesced loads    */
-    SHA1CHUNK_KERNEL_SPLIT = 3  /* schedule-producer + round-consumer wave pairs      */
+    SHA1CHUNK_KERNEL_LANE = 1,  /* one lane per chunk, per-lane loads; any alignment   */
+    SHA1CHUNK_KERNEL_FUSED = 2, /* one lane per chunk, schedule + rounds in registers,
+                                   two 128-byte stages of per-lane 16-byte loads ahead */
+    SHA1CHUNK_KERNEL_SPLIT = 3  /* schedule-producer + round-consumer wave pairs        */
 };
 
 /* digests[i*20 .. i*20+19] = SHA-1(base[offsets[i] .. offsets[i]+lengths[i])).
