@@ -600,7 +600,7 @@ int sha1chunk_get_device(void) { return t_dev; }
 
 const char* sha1chunk_last_error(void) { return t_err.c_str(); }
 
-const char* sha1chunk_version(void) { return "sha1chunk gfx950: lane,fused,split"; }
+const char* sha1chunk_version(void) { return "sha1chunk gfx950: lane,fused,split,mixed"; }
 
 int sha1chunk_hash_device_async(const void* d_base, const uint64_t* d_offsets,
                                 const uint32_t* d_lengths, size_t n, uint8_t* d_digests,
