@@ -52,9 +52,12 @@ def main():
     ap.add_argument("--chunks", default="16384,65536,131072")
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--modes", default="auto,auto_nomixed,split4_sorted")
-    ap.add_argument("--layout", default="arrival", choices=["arrival", "sorted", "shuffled"],
-                    help="chunk placement in memory: arrival order, sorted longest-first, or "
-                         "arrival order with the offsets permuted at random")
+    ap.add_argument("--layout", default="arrival",
+                    choices=["arrival", "sorted", "shuffled", "shuffled_blocks4", "shuffled_window64"],
+                    help="chunk placement in memory: arrival order, sorted longest-first, "
+                         "arrival order with the offsets permuted at random, permuted in runs of 4 "
+                         "adjacent chunks (2 MiB for 512 KiB chunks), or permuted only within each "
+                         "window of 64 chunks")
     ap.add_argument("--uniform", type=int, default=0, help="every chunk this long instead of the law")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
@@ -68,8 +71,14 @@ def main():
         if a.layout == "sorted":
             lens = np.sort(lens)[::-1].copy()
         off, total = pkg.sha1chunk.ragged_layout(lens)
-        if a.layout == "shuffled":
-            perm = np.random.default_rng(1).permutation(n)
+        if a.layout.startswith("shuffled"):
+            rng = np.random.default_rng(1)
+            if a.layout == "shuffled":
+                perm = rng.permutation(n)
+            elif a.layout == "shuffled_blocks4":
+                perm = (rng.permutation(n // 4)[:, None] * 4 + np.arange(4)[None, :]).reshape(-1)
+            else:
+                perm = np.concatenate([w + rng.permutation(min(64, n - w)) for w in range(0, n, 64)])
             off, lens = off[perm].copy(), lens[perm].copy()
         base = torch.zeros(total + 128, dtype=torch.uint8, device="cuda")
         d_off = torch.from_numpy(off.astype(np.int64)).cuda()
