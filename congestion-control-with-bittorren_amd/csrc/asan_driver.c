@@ -19,6 +19,13 @@
 
 #define L512 524288u
 
+/* the few HIP runtime calls the device-batch section needs (C linkage in
+ * libamdhip64; hipMemcpyKind 1 = host to device, 2 = device to host) */
+extern int hipMalloc(void **p, size_t bytes);
+extern int hipFree(void *p);
+extern int hipMemcpy(void *dst, const void *src, size_t bytes, int kind);
+extern int hipDeviceSynchronize(void);
+
 static int fails = 0;
 #define CHECK(c, ...)                                   \
     do {                                                \
@@ -118,6 +125,53 @@ int main(void) {
     }
     CHECK(seen == n && sha1chunk_vq_pending(q) == 0, "vq drained %zu of %zu", seen, n);
     sha1chunk_vq_destroy(q);
+
+    /* device ragged batch above one group per CU: the length sort, the
+     * mixed kernel's planner and its forced plans (env parsing included),
+     * against the host batch path; a malformed plan must fail */
+    {
+        const size_t nd = 64 * 320 + 17; /* > 256 CUs' worth of groups */
+        uint64_t *doff = malloc(nd * sizeof *doff);
+        uint32_t *dlen = malloc(nd * sizeof *dlen);
+        size_t dtot = 0;
+        for (size_t i = 0; i < nd; ++i) {
+            dlen[i] = (i % 97 == 0) ? 20000u + (uint32_t)(i % 300u) : (uint32_t)((i * 2654435761u) % 1500u);
+            doff[i] = dtot;
+            dtot += (dlen[i] + 127u) / 128u * 128u;
+        }
+        uint8_t *hb = malloc(dtot + 64);
+        for (size_t i = 0; i < dtot + 64; ++i) hb[i] = next_byte();
+        uint8_t *want = malloc(nd * 20), *gotd = malloc(nd * 20);
+        CHECK(sha1chunk_hash_batch(hb, doff, dlen, nd, want, SHA1CHUNK_HOST) == 0, "host ragged: %s",
+              sha1chunk_last_error());
+        void *dbase = NULL, *doffp = NULL, *dlenp = NULL, *ddig = NULL;
+        CHECK(!hipMalloc(&dbase, dtot + 64) && !hipMalloc(&doffp, nd * 8) && !hipMalloc(&dlenp, nd * 4) &&
+                  !hipMalloc(&ddig, nd * 20),
+              "hipMalloc");
+        CHECK(!hipMemcpy(dbase, hb, dtot + 64, 1) && !hipMemcpy(doffp, doff, nd * 8, 1) &&
+                  !hipMemcpy(dlenp, dlen, nd * 4, 1),
+              "hipMemcpy H2D");
+        static const char *plans[] = {NULL, "0,0,4", "0,0,8", "0,7,4", "0,321,4", "1,0,0"};
+        for (size_t k = 0; k < sizeof plans / sizeof plans[0]; ++k) {
+            if (plans[k]) setenv("SHA1CHUNK_MIXED_PLAN", plans[k], 1);
+            else unsetenv("SHA1CHUNK_MIXED_PLAN");
+            setenv("SHA1CHUNK_MIXED_DEBUG", k == 0 ? "1" : "0", 1);
+            memset(gotd, 0, nd * 20);
+            CHECK(sha1chunk_hash_device_async(dbase, doffp, dlenp, nd, ddig, NULL, SHA1CHUNK_KERNEL_AUTO) == 0,
+                  "device ragged plan %s: %s", plans[k] ? plans[k] : "device", sha1chunk_last_error());
+            CHECK(!hipDeviceSynchronize() && !hipMemcpy(gotd, ddig, nd * 20, 2), "device sync");
+            CHECK(!memcmp(gotd, want, nd * 20), "device ragged plan %s differs", plans[k] ? plans[k] : "device");
+        }
+        setenv("SHA1CHUNK_MIXED_PLAN", "0,99999,4", 1);
+        CHECK(sha1chunk_hash_device_async(dbase, doffp, dlenp, nd, ddig, NULL, SHA1CHUNK_KERNEL_AUTO) ==
+                  SHA1CHUNK_EINVAL,
+              "bad plan accepted");
+        unsetenv("SHA1CHUNK_MIXED_PLAN");
+        unsetenv("SHA1CHUNK_MIXED_DEBUG");
+        hipDeviceSynchronize();
+        hipFree(dbase), hipFree(doffp), hipFree(dlenp), hipFree(ddig);
+        free(doff), free(dlen), free(hb), free(want), free(gotd);
+    }
 
     /* file pipeline: make_chunks(FILE*) and the fd path over a temp file */
     char path[] = "/tmp/asan_driver_XXXXXX";

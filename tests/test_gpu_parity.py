@@ -435,7 +435,8 @@ def test_host_batch_all_devices(pkg, dev, oracle, golden):
 def test_host_paths_under_asan(pkg, dev):
     """Every host path of the library (batch pipelines, pinned staging, part
     pools, verify queue with growth, streaming trio, make_chunks(FILE*),
-    get_chunk_hash/verify_hash) under host AddressSanitizer + UBSan
+    get_chunk_hash/verify_hash, the device ragged path's sort and mixed-kernel
+    planning with forced and malformed plans) under host AddressSanitizer + UBSan
     (`make asan`: csrc/asan_driver.c against build-asan/libsha1chunk.so,
     built on the CPU beforehand like every other binary).  Device code is
     not instrumented; any host report makes the driver exit non-zero."""
