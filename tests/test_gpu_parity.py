@@ -51,6 +51,19 @@ def test_kats_streaming_trio(pkg, dev, golden):
     assert s.final().hex() == golden["kats"]["million_a"]["digest"]
 
 
+def test_final_64bit_bit_count(pkg, dev, oracle):
+    """SHA1Final on contexts of >= 4 GiB messages (the 64-bit bit count's
+    high word non-zero, sha.c:540-543; up to 2^61 bytes) through the device
+    finish kernel: digest and the context left behind equal the reference
+    sha.c's (oracle/_ref; the restatement where it was not built)."""
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    from test_oracle import _final, long_message_contexts
+    ref = oracle.ref_lib()
+    want_fn = ref.SHA1Final if ref is not None else oracle.lib().oracle_sha1_final
+    for ctx in long_message_contexts():
+        assert _final(pkg.lib().SHA1Final, ctx) == _final(want_fn, ctx), ctx.totalLength
+
+
 @pytest.mark.parametrize("kernel", ["auto", "lane", "fused", "split"])
 def test_streaming_odd_splits(pkg, dev, oracle, kernel, monkeypatch):
     """SHA1Update/SHA1Final (sha.c:453-558) with the device compressing the

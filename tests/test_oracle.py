@@ -1,5 +1,6 @@
 """CPU: pin the oracle (oracle/sha1_oracle.c) against the reference's own
 known answers and fixtures, and against the compiled reference sha.c."""
+import ctypes
 import hashlib
 import os
 
@@ -117,3 +118,49 @@ def test_restatement_matches_reference_build(oracle):
     a = oracle.hash_batch(buf, off, lens, threads=4)
     b = oracle.hash_batch(buf, off, lens, threads=4, use_ref=True)
     assert np.array_equal(a, b)
+
+
+class _Ctx(ctypes.Structure):
+    """SHA1Context (sha.h:39-52), 96 bytes."""
+    _fields_ = [("totalLength", ctypes.c_uint64), ("hash", ctypes.c_uint32 * 5),
+                ("bufferLength", ctypes.c_uint32), ("buffer", ctypes.c_uint8 * 64)]
+
+
+def long_message_contexts(seed=3):
+    """Consistent mid-stream contexts whose message is >= 2^32 bytes long, so
+    the 64-bit big-endian bit count SHA1Final appends (sha.c:540-543) has a
+    non-zero high word: K whole blocks already compressed, r bytes staged."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for K in (1 << 26, 5 * (1 << 26) + 3, (1 << 40) + 12345, (1 << 55) - 1):
+        for r in (0, 1, 55, 56, 63):
+            c = _Ctx()
+            c.totalLength = 8 * (64 * K + r)
+            for i, w in enumerate(rng.integers(0, 1 << 32, 5, dtype=np.uint64)):
+                c.hash[i] = int(w)
+            c.bufferLength = r
+            for i, b in enumerate(rng.integers(0, 256, 64, dtype=np.uint8)):
+                c.buffer[i] = int(b)
+            out.append(c)
+    return out
+
+
+def _final(fn, ctx):
+    """Call a SHA1Final-shaped C function on a copy of ctx (a private
+    prototype, so the library's own ctypes bindings are left alone)."""
+    c = _Ctx.from_buffer_copy(bytes(ctx))
+    d = (ctypes.c_uint8 * 20)()
+    f = ctypes.cast(fn, ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.c_void_p))
+    f(ctypes.addressof(c), ctypes.addressof(d))
+    return bytes(d), (c.totalLength, tuple(c.hash), c.bufferLength)
+
+
+def test_final_64bit_bit_count_vs_reference(oracle):
+    """The restatement's SHA1Final against the reference sha.c's on contexts
+    of >= 4 GiB messages (bit count >= 2^35): same digest, same context left
+    behind (chaining value, padded length, nothing staged)."""
+    ref = oracle.ref_lib()
+    if ref is None:
+        pytest.skip("oracle/_ref not built (no /root/reference here)")
+    for ctx in long_message_contexts():
+        assert _final(oracle.lib().oracle_sha1_final, ctx) == _final(ref.SHA1Final, ctx), ctx.totalLength
