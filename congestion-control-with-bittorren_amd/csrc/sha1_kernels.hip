@@ -29,6 +29,10 @@
 //                      SIMD to itself (a workgroup's waves 0-3 land on four
 //                      different SIMDs, wave w + 4 on wave w's:
 //                      tools/wave_placement_probe.hip).
+//   sha1_mixed_kernel  ragged batches sorted longest-first with more groups
+//                      than CUs: one launch whose workgroups run the split
+//                      body (longest groups) or the fused body, per a
+//                      device-side plan (plan_mixed_kernel) -- see `mixed`.
 //
 // Measured on MI355X (tools/issue_probe.hip, tools/gen_consumer_probe.py,
 // DESIGN.md section 5): one wave issues at most one instruction per 4.0
