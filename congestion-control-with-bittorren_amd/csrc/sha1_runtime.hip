@@ -316,9 +316,10 @@ bool use_mixed() {
 }
 
 // SHA1CHUNK_MIXED_PLAN="mode,H,F" replaces the device-side plan (tests and
-// A/B runs): mode 0 with 0 <= H <= min(groups, 4 CUs) and F in {4, 8}, or
-// mode 1.  SHA1CHUNK_MIXED_DEBUG=1 prints the plan used (synchronises the
-// stream: diagnostics only).
+// A/B runs): mode 0 with H <= the model's head cap (min(groups, 4 CUs,
+// 4096)) or H = groups, and F in {4, 8}; or mode 1.
+// SHA1CHUNK_MIXED_DEBUG=1 prints the plan used (synchronises the stream:
+// diagnostics only).
 int launch_mixed_checked(const BatchArgs& A, const uint32_t* sorted_len, uint32_t* plan, int cus,
                          hipStream_t st) {
     if (A.n > 0 && (reinterpret_cast<uintptr_t>(A.dig) & 3u))
@@ -327,7 +328,8 @@ int launch_mixed_checked(const BatchArgs& A, const uint32_t* sorted_len, uint32_
     bool force = false;
     if (const char* e = getenv("SHA1CHUNK_MIXED_PLAN")) {
         uint32_t hcap;
-        const uint32_t groups = (A.n + 63u) / 64u, grid = mixed_grid(groups, cus, &hcap);
+        const uint32_t groups = (A.n + 63u) / 64u;
+        (void)mixed_grid(groups, cus, &hcap);
         if (sscanf(e, "%d,%d,%d", &forced[0], &forced[1], &forced[2]) != 3 || forced[0] < 0 ||
             forced[0] > 1 ||
             (forced[0] == 0 && (forced[1] < 0 || ((uint32_t)forced[1] > hcap && (uint32_t)forced[1] != groups) ||
@@ -335,7 +337,6 @@ int launch_mixed_checked(const BatchArgs& A, const uint32_t* sorted_len, uint32_
             return fail(SHA1CHUNK_EINVAL,
                         "SHA1CHUNK_MIXED_PLAN=%s: want 0,H,F (0 <= H <= %u or H = %u, F 4|8) or 1,0,0", e,
                         hcap, groups);
-        (void)grid;
         force = true;
     }
     hipError_t e = launch_mixed(A, sorted_len, plan, cus, force ? forced : nullptr, st);
