@@ -73,3 +73,46 @@ def test_random_batches_every_kernel(pkg, dev, oracle, seed, monkeypatch):
     # the host-memory path (pageable numpy): packing + pipeline
     got = pkg.hash_batch(host, off, lens)
     assert np.array_equal(got, want), f"seed {seed}: host batch"
+
+
+# The mixed kernel (more groups of 64 than CUs, AUTO on a ragged device
+# batch): random batches of mostly short chunks with a few long ones, in
+# caller order or scrambled, each through the device plan, two random forced
+# mode-0 plans and the 8-wave mode.
+@pytest.mark.parametrize("seed", range(int(os.environ.get("SHA1CHUNK_FUZZ_SEEDS", "12")) // 3 + 1))
+def test_random_batches_mixed_kernel(pkg, dev, oracle, seed, monkeypatch):
+    torch = dev
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    rng = np.random.default_rng(9100 + seed)
+    G = int(rng.integers(cus + 1, 5 * cus))
+    n = 64 * G - int(rng.integers(0, 64))
+    lens = _lengths(rng, n) % 4000
+    lens[rng.choice(n, int(rng.integers(1, 3 * cus)), replace=False)] = rng.integers(20000, 90000)
+    align = int(rng.choice([1, 16, 64]))
+    step = (lens.astype(np.uint64) + np.uint64(align - 1)) // np.uint64(align) * np.uint64(align)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum(step)[: n - 1]
+    if rng.integers(0, 2):  # caller order scrambled: scattered groups
+        perm = rng.permutation(n)
+        off, lens = off[perm].copy(), lens[perm].copy()
+    host = rng.integers(0, 256, int(off.max() + 90000) + 64, dtype=np.uint8)
+    want = oracle.hash_batch(host, off, lens)
+    d_host = torch.from_numpy(host).cuda()
+    d_off = torch.from_numpy(off.astype(np.int64)).cuda()
+    d_len = torch.from_numpy(lens.astype(np.int32)).cuda()
+    hcap = min(G, 4 * cus, 4096)
+    plans = [None] + [f"0,{int(rng.choice([0, int(rng.integers(0, hcap + 1)), hcap, G]))},"
+                      f"{int(rng.choice([4, 8]))}" for _ in range(2)] + ["1,0,0"]
+    for p in plans:
+        if p is None:
+            monkeypatch.delenv("SHA1CHUNK_MIXED_PLAN", raising=False)
+        else:
+            monkeypatch.setenv("SHA1CHUNK_MIXED_PLAN", p)
+        dig = torch.zeros((n, 20), dtype=torch.uint8, device="cuda")
+        pkg.hash_device(d_host, d_off, d_len, dig)
+        torch.cuda.synchronize()
+        got = dig.cpu().numpy()
+        bad = np.nonzero((got != want).any(axis=1))[0]
+        assert bad.size == 0, f"seed {seed} plan {p or 'device'} n={n} align={align}: {bad.size} bad, " \
+                              f"first {bad[:6]} lens {lens[bad[:6]]}"
+    monkeypatch.delenv("SHA1CHUNK_MIXED_PLAN", raising=False)
