@@ -678,13 +678,15 @@ __global__ __launch_bounds__(256) void sha1_fused_kernel(BatchArgs A) {
 // (the all-split plan); workgroups past a plan's count exit at once.
 //
 // Memory locality decides as much as the model below: every lane streams
-// its own chunk, so the chip keeps one address translation per chunk in
-// flight, and when a group's 64 chunks lie far apart (a sorted batch whose
-// chunks arrived in random length order) the fused tail's many resident
-// chunks thrash them: 65536 x 512 KiB with permuted offsets hash in 28.9 ms
-// fused against 10.6 ms in place, and the config-5 law at 65536 chunks in
-// arrival order runs its all-fused plan at 1.98 us per block against 1.28
-// for the same lengths laid out longest-first (profiles/mixed_r02.json).
+// its own chunk, and when the resident chunks lie far apart (a sorted batch
+// whose chunks arrived in random length order) the memory system slows
+// down with their number -- which lane reads which chunk does not matter,
+// how far apart the regions they touch lie does (tools/locality_probe.sh;
+// address translation is the likely cause).  65536 x 512 KiB with permuted
+// offsets hash in 28.9 ms fused against 10.6 ms in place, and the config-5
+// law at 65536 chunks in arrival order runs its all-fused plan at 1.98 us
+// per block against 1.28 for the same lengths laid out longest-first
+// (profiles/mixed_r02.json).
 // The planner therefore sends a scattered batch (most of its work in
 // groups whose chunks span more than 4x their bytes + 4 MiB of address
 // space) to the one-group split shape whole: a quarter of the resident
