@@ -679,10 +679,11 @@ __global__ __launch_bounds__(256) void sha1_fused_kernel(BatchArgs A) {
 //
 // Memory locality decides as much as the model below: every lane streams
 // its own chunk, and when the resident chunks lie far apart (a sorted batch
-// whose chunks arrived in random length order) the memory system slows
-// down with their number -- which lane reads which chunk does not matter,
-// how far apart the regions they touch lie does (tools/locality_probe.sh;
-// address translation is the likely cause).  65536 x 512 KiB with permuted
+// whose chunks arrived in random length order) the CU's translation cache
+// (UTCL1) thrashes: 98 % misses instead of ~0 on the same requests, L2
+// unchanged (tools/tlb_probe.sh, profiles/tlb_r02.json) -- which lane reads
+// which chunk does not matter, how far apart the regions they touch lie
+// does (tools/locality_probe.sh).  65536 x 512 KiB with permuted
 // offsets hash in 28.9 ms fused against 10.6 ms in place, and the config-5
 // law at 65536 chunks in arrival order runs its all-fused plan at 1.98 us
 // per block against 1.28 for the same lengths laid out longest-first
