@@ -689,9 +689,9 @@ __global__ __launch_bounds__(256) void sha1_fused_kernel(BatchArgs A) {
 // per block against 1.28 for the same lengths laid out longest-first
 // (profiles/mixed_r02.json).
 // The planner therefore sends a scattered batch (most of its work in
-// groups whose chunks span more than 4x their bytes + 4 MiB of address
-// space) to the one-group split shape whole: a quarter of the resident
-// chunks per CU of the fused tail, and the shortest chains.
+// groups whose chunks touch well over the 2 MiB pages their bytes need,
+// group_scattered) to the one-group split shape whole: a quarter of the
+// resident chunks per CU of the fused tail, and the shortest chains.
 constexpr int kSplit8V = kVWK | kVUnmask | kVLayout8 | kVCross;
 constexpr int kMixedThreads = 512;
 
@@ -776,19 +776,73 @@ __device__ double makespan(const uint32_t* sorted_len, uint32_t G, uint32_t C, u
 constexpr int kPlanThreads = 1024;
 constexpr uint32_t kPlanMaxH = 4096;  // largest split head the model search considers
 
-// Whether group g's chunks lie close together: their address span (first
-// byte to last) against their bytes.
-__device__ __forceinline__ bool group_scattered(const BatchArgs& A, uint32_t g) {
-    uint64_t lo = ~0ull, hi = 0, bytes = 0;
-    const uint32_t e1 = min(A.n, 64u * g + 64u);
-    for (uint32_t e = 64u * g; e < e1; ++e) {
-        const uint32_t id = A.order[e];
-        const uint64_t o = A.off[id], l = A.len[id];
-        lo = min(lo, o);
-        hi = max(hi, o + l);
-        bytes += l;
+// Whether group g's chunks are spread over many translation regions: one
+// wave (lane = chunk) counts the distinct 2 MiB pages holding the chunks'
+// first bytes against the fewest pages the group's bytes could fill;
+// scattered above 1.5x that + 1.  Chunks in place in caller order (4 per
+// page at 512 KiB: 16 pages for 16) or in runs sharing pages are not; a
+// longest-first order of chunks that arrived in random length order is (64
+// pages for 1 MiB chunks that would fill 32, for 512 KiB ones 16, for 4 KiB
+// ones 1).  Measured on 65536 x 512 KiB: in place the fused kernel takes
+// 10.6 ms, with the 2 MiB runs scattered 14.8 (still ahead of the split
+// shape's 24.6), with every chunk on a page of its own 29.3 (the split
+// shape: 28.9) -- profiles/mixed_r02.json.
+__device__ __forceinline__ bool group_scattered(uint32_t page, uint32_t kib, bool valid, uint32_t lane) {
+    // lane k's page and size through v_readlane (VALU + scalar adds, no LDS
+    // traffic: the planner is one workgroup on one CU)
+    uint32_t dup = 0, total_kib = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 64; ++k) {
+        const uint32_t other = __builtin_amdgcn_readlane(page, k);
+        total_kib += __builtin_amdgcn_readlane(kib, k);
+        dup |= (uint32_t)(lane > k) & (uint32_t)(other == page);
     }
-    return hi > lo && hi - lo > 4ull * bytes + (4ull << 20);
+    const uint32_t distinct = (uint32_t)__popcll(__ballot(valid && !dup));
+    const uint32_t fill = (total_kib + 2047u) / 2048u;  // 2 MiB pages the bytes fill at the least
+    return 2u * distinct > 3u * fill + 2u;
+}
+
+// The scatter test runs on a sample of groups spread evenly over the
+// batch (sample i is group i * G / S, S = min(G, kScatterSample)): the
+// decision is a work-weighted fraction, and the test costs ~200
+// instructions per group on the planner's one CU (every group of a
+// 4096-group batch through LDS shuffles took ~0.8 ms).  One wave takes
+// samples first, first + step, .., their chunk loads kScatterBatch groups at
+// once; returns {work in scattered sampled groups, work in all sampled
+// groups}.
+constexpr uint32_t kScatterBatch = 8, kScatterSample = 256;
+struct FarWork {
+    uint64_t far, all;
+};
+__device__ FarWork scattered_work(const BatchArgs& A, const uint32_t* sorted_len, uint32_t G, uint32_t first,
+                                  uint32_t step, uint32_t lane) {
+    const uint32_t S = min(G, kScatterSample);
+    FarWork w{0, 0};
+    for (uint32_t i0 = first; i0 < S; i0 += kScatterBatch * step) {
+        uint32_t gs[kScatterBatch], id[kScatterBatch], page[kScatterBatch], kib[kScatterBatch];
+        bool valid[kScatterBatch];
+#pragma unroll
+        for (uint32_t j = 0; j < kScatterBatch; ++j) {
+            const uint32_t i = i0 + j * step;
+            gs[j] = i < S ? (uint32_t)((uint64_t)i * G / S) : G;
+            const uint64_t e = 64ull * gs[j] + lane;
+            valid[j] = gs[j] < G && e < A.n;
+            id[j] = valid[j] ? A.order[e] : 0u;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kScatterBatch; ++j) {
+            page[j] = valid[j] ? (uint32_t)(A.off[id[j]] >> 21) : 0xffffffffu - lane;
+            kib[j] = valid[j] ? (uint32_t)(((uint64_t)A.len[id[j]] + 1023u) >> 10) : 0u;
+        }
+#pragma unroll
+        for (uint32_t j = 0; j < kScatterBatch; ++j) {
+            if (gs[j] >= G) continue;
+            const uint32_t b = group_blocks(sorted_len, gs[j]);
+            w.all += b;
+            if (group_scattered(page[j], kib[j], valid[j], lane)) w.far += b;
+        }
+    }
+    return w;
 }
 
 __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, const uint32_t* sorted_len,
@@ -812,16 +866,20 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     const uint32_t G = (n + 63u) / 64u;
     const uint32_t per = (G + kPlanThreads - 1) / kPlanThreads;
     const uint32_t g0 = min(G, t * per), g1 = min(G, g0 + per);
-    uint64_t local = 0, local_far = 0;
-    for (uint32_t g = g0; g < g1; ++g) {
-        const uint32_t b = group_blocks(sorted_len, g);
-        local += b;
-        if (group_scattered(A, g)) local_far += b;
-    }
-    __shared__ uint64_t far_sum;
-    if (t == 0) far_sum = 0;
+    uint64_t local = 0;
+    for (uint32_t g = g0; g < g1; ++g) local += group_blocks(sorted_len, g);
+    // work in scattered groups (sampled): wave w takes samples w, w + 16, ..
+    __shared__ uint64_t far_sum, sampled_sum;
+    if (t == 0) far_sum = sampled_sum = 0;
     __syncthreads();
-    if (local_far) atomicAdd(reinterpret_cast<unsigned long long*>(&far_sum), (unsigned long long)local_far);
+    {
+        const uint32_t lane = t & 63u, wave = t >> 6, waves = kPlanThreads / 64;
+        const FarWork w = scattered_work(A, sorted_len, G, wave, waves, lane);
+        if (lane == 0 && w.all) {
+            atomicAdd(reinterpret_cast<unsigned long long*>(&far_sum), (unsigned long long)w.far);
+            atomicAdd(reinterpret_cast<unsigned long long*>(&sampled_sum), (unsigned long long)w.all);
+        }
+    }
     scan[t] = local;
     __syncthreads();
     for (uint32_t off = 1; off < kPlanThreads; off <<= 1) {
@@ -831,7 +889,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         __syncthreads();
     }
     const uint64_t PG = scan[kPlanThreads - 1];
-    if (2 * far_sum > PG) {  // scattered: every group in the one-group split shape
+    if (2 * far_sum > sampled_sum) {  // scattered: every group in the one-group split shape
         if (t == 0) {
             plan[0] = 0;
             plan[1] = G;

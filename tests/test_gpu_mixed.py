@@ -65,17 +65,27 @@ def model_makespan(B, C, mode, H, F, P):
     return m
 
 
+SCATTER_SAMPLE = 256
+
+
 def scattered_work(order, off, lens, B):
-    """plan_mixed_kernel's locality test, restated: the share of the work in
-    groups whose chunks span more than 4x their bytes + 4 MiB."""
-    far = 0
-    for g, b in enumerate(B):
+    """plan_mixed_kernel's locality test (group_scattered on the sample
+    scattered_work takes), restated: (work in sampled groups whose chunks
+    start in more distinct 2 MiB pages than 1.5x the pages their bytes fill
+    + 1, work in all sampled groups)."""
+    G = len(B)
+    S = min(G, SCATTER_SAMPLE)
+    far = tot = 0
+    for i in range(S):
+        g = i * G // S
         ids = order[64 * g:64 * g + 64]
-        o, ln = off[ids].astype(np.int64), lens[ids].astype(np.int64)
-        span = int((o + ln).max() - o.min())
-        if span > 4 * int(ln.sum()) + (4 << 20):
-            far += b
-    return far
+        pages = np.unique(off[ids].astype(np.uint64) >> np.uint64(21)).size
+        kib = int(((lens[ids].astype(np.int64) + 1023) >> 10).sum())
+        fill = (kib + 2047) // 2048
+        tot += B[g]
+        if 2 * pages > 3 * fill + 2:
+            far += B[g]
+    return far, tot
 
 
 def model_plan(lengths, C, off=None):
@@ -88,7 +98,8 @@ def model_plan(lengths, C, off=None):
     P = [0]
     for b in B:
         P.append(P[-1] + b)
-    if off is not None and 2 * scattered_work(order, off, lengths, B) > P[G]:
+    far, tot = scattered_work(order, off, lengths, B) if off is not None else (0, 1)
+    if 2 * far > tot:
         return (model_makespan(B, C, 0, G, 4, P), 0, G, 4), (B, P)
     hcap, grid = grid_of(G, C)
     best = None

@@ -88,3 +88,27 @@ def test_model_rounds_bound_is_exact_for_equal_jobs():
         P.append(P[-1] + b)
     m = M.model_makespan(B, C, 1, 0, 0, P)
     assert m == pytest.approx(2 * 1025 * M.CHAIN["split8"])
+
+
+@pytest.mark.parametrize("layout,scattered", [("in_place", False), ("window64", False),
+                                              ("runs_of_4", False), ("random", True)])
+def test_uniform_layouts_scatter_rule(layout, scattered):
+    """65536 x 512 KiB laid out as tools/locality_probe.sh measured them: in
+    place, permuted within each 64-chunk window, permuted in 2 MiB runs of
+    four (fused 14.8 ms, split 24.6: keep the fused kernel), permuted at
+    random (fused 29.3, split 28.9: the split shape)."""
+    n = 65536
+    lens = np.full(n, L512, np.uint32)
+    off = contiguous(lens)
+    rng = np.random.default_rng(1)
+    if layout == "window64":
+        perm = np.concatenate([w + rng.permutation(64) for w in range(0, n, 64)])
+    elif layout == "runs_of_4":
+        perm = (rng.permutation(n // 4)[:, None] * 4 + np.arange(4)[None, :]).reshape(-1)
+    elif layout == "random":
+        perm = rng.permutation(n)
+    else:
+        perm = np.arange(n)
+    off = off[perm]
+    (est, m, H, F), (B, _) = M.model_plan(lens, C, off)
+    assert ((m, H, F) == (0, len(B), 4)) == scattered, (layout, m, H, F)
