@@ -653,6 +653,112 @@ __global__ __launch_bounds__(256) void sha1_fused_kernel(BatchArgs A) {
     fused_body<RV>(A, blockIdx.x * 256u + threadIdx.x);
 }
 
+// ---------------------------------------------------------- coop fused ----
+// The fused wave with its bulk loads shared across the wave: instruction i
+// (i = 0..7) of a 128-byte stage reads 128 bytes of each of the group's
+// chunks 8i .. 8i+7 (lane l: chunk 8i + l/8, 16-byte piece l%8), so one load
+// instruction touches 8 chunks instead of 64, and an LDS transpose hands
+// each lane its own chunk's 128 bytes.  The lane-per-chunk pattern makes
+// each load instruction translate 64 addresses; with chunks far apart that
+// thrashes the CU's translation cache: scattered 512 KiB chunks read at
+// 1183 GB/s lane-per-chunk and 5954 GB/s 8 chunks per instruction (5036 /
+// 5980 in place; tools/coop_probe.hip).  Used by the mixed kernel, whose
+// workgroups own the CU's LDS anyway (16 KiB per wave: two stage buffers).
+// Swizzle: piece p of chunk c at c*128 + ((p + c/2) & 7)*16, conflict-free
+// for the b128 stores (8 contiguous lanes write one chunk) and for the b128
+// reads (each of ds_read_b128's 16-lane groups sees 16 distinct 16-byte
+// bank groups).
+constexpr uint32_t kCoopStageBytes = 64u * 128u;
+constexpr uint32_t kCoopWaveBytes = 2u * kCoopStageBytes;
+
+__device__ __forceinline__ uint32_t coop_slot(uint32_t c, uint32_t piece) {
+    return c * 128u + ((piece + (c >> 1)) & 7u) * 16u;
+}
+
+// (the in-flight stage lives in plain 32-bit words: an array of uint4
+// stays in scratch memory)
+__device__ __forceinline__ void coop_load(const uint4* const (&src)[8], uint32_t s, uint32_t (&v)[32]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint4 x = src[i][8u * s];
+        v[4 * i + 0] = x.x;
+        v[4 * i + 1] = x.y;
+        v[4 * i + 2] = x.z;
+        v[4 * i + 3] = x.w;
+    }
+}
+
+__device__ __forceinline__ void coop_store(uint8_t* buf, const uint32_t (&v)[32], uint32_t lane) {
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i)
+        *reinterpret_cast<uint4*>(buf + coop_slot(8u * i + lane / 8u, lane & 7u)) =
+            make_uint4(v[4 * i + 0], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+}
+
+__device__ __forceinline__ void coop_read(const uint8_t* buf, uint32_t lane, uint32_t (&w)[32]) {
+#pragma unroll
+    for (uint32_t p = 0; p < 8; ++p) {
+        const uint4 x = *reinterpret_cast<const uint4*>(buf + coop_slot(lane, p));
+        w[4 * p + 0] = x.x;
+        w[4 * p + 1] = x.y;
+        w[4 * p + 2] = x.z;
+        w[4 * p + 3] = x.w;
+    }
+}
+
+// lds: this wave's kCoopWaveBytes.  Same contract as fused_body.
+template <int RV>
+__device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, uint8_t* lds) {
+    const uint32_t group = e / 64u, lane = e & 63u;
+    const bool valid = e < A.n;
+    Entry en = fetch_entry(A, valid ? e : min(group * 64u, A.n - 1u));
+    if (!valid) en.len = 0;
+    uint32_t h[5];
+    load_init(A, en.id, h);
+    const bool a16 = (reinterpret_cast<uintptr_t>(en.p) & 15u) == 0;
+    const uint32_t S = (wave_any(valid) && wave_all(!valid || a16))
+                           ? __builtin_amdgcn_readfirstlane(
+                                 wave_min(valid ? (en.len >> 7) : 0xffffffffu))
+                           : 0u;
+    if (S > 0) {
+        // this lane's piece of chunks 8i + lane/8; a slot past the batch
+        // reads the group's first chunk (valid, and at least S stages long)
+        const uint4* src[8];
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i) {
+            const uint32_t ej = group * 64u + 8u * i + lane / 8u;
+            src[i] = reinterpret_cast<const uint4*>(fetch_entry(A, ej < A.n ? ej : group * 64u).p) + (lane & 7u);
+        }
+        // stage loads run ahead unconditionally (clamped to the last stage:
+        // a repeated read at the end, never past a chunk)
+        uint32_t v[32];
+        coop_load(src, 0, v);
+        coop_store(lds, v, lane);
+        coop_load(src, min(1u, S - 1u), v);
+        for (uint32_t s = 0; s < S; ++s) {
+            // LDS operations of one wave complete in order: this stage's
+            // stores (last iteration) precede these reads, and the next
+            // stage's stores follow them; hipcc keeps the program order of
+            // LDS accesses it cannot prove disjoint (these are lane-dependent).
+            uint32_t cur[32];
+            coop_read(lds + (s & 1u) * kCoopStageBytes, lane, cur);
+            coop_store(lds + ((s + 1u) & 1u) * kCoopStageBytes, v, lane);
+            coop_load(src, min(s + 2u, S - 1u), v);
+#pragma unroll
+            for (int half = 0; half < 2; ++half) {
+                uint32_t w[16];
+#pragma unroll
+                for (int j = 0; j < 16; ++j) w[j] = bswap(cur[16 * half + j]);
+                compress<RV>(h, w);
+            }
+        }
+    }
+    if (valid) {
+        lane_blocks(A, en, 2u * S, h);
+        emit(A, en.id, h);
+    }
+}
+
 // --------------------------------------------------------------- mixed ----
 // Ragged batches with more groups of 64 than CUs, sorted longest-first
 // (BASELINE config 5's shape beyond 16384 chunks).  A batch of mixed lengths
@@ -669,7 +775,8 @@ __global__ __launch_bounds__(256) void sha1_fused_kernel(BatchArgs A) {
 //           CU in the one-group split shape (4-block units, two producers,
 //           the consumer alone on its SIMD); workgroup H + j hashes groups
 //           H + j*F .. H + j*F + F-1 fused, one group per wave (F = 4: one
-//           wave per SIMD, chain 1.28 us per block; F = 8: two).
+//           wave per SIMD, chain 1.28 us per block; F = 8: two), the stage
+//           loads shared across the wave (fused_coop_body).
 //   mode 1: workgroup w hashes groups 2w, 2w+1 in the 8-wave two-pair split
 //           shape (AUTO's shape for C < groups <= 2C on a uniform batch).
 // Blocks in dispatch order: the longest groups start first, and the
@@ -677,21 +784,17 @@ __global__ __launch_bounds__(256) void sha1_fused_kernel(BatchArgs A) {
 // (longest-processing-time order).  The grid is one workgroup per group
 // (the all-split plan); workgroups past a plan's count exit at once.
 //
-// Memory locality decides as much as the model below: every lane streams
-// its own chunk, and when the resident chunks lie far apart (a sorted batch
-// whose chunks arrived in random length order) the CU's translation cache
-// (UTCL1) thrashes: 98 % misses instead of ~0 on the same requests, L2
-// unchanged (tools/tlb_probe.sh, profiles/tlb_r02.json) -- which lane reads
-// which chunk does not matter, how far apart the regions they touch lie
-// does (tools/locality_probe.sh).  65536 x 512 KiB with permuted
-// offsets hash in 28.9 ms fused against 10.6 ms in place, and the config-5
-// law at 65536 chunks in arrival order runs its all-fused plan at 1.98 us
-// per block against 1.28 for the same lengths laid out longest-first
-// (profiles/mixed_r02.json).
-// The planner therefore sends a scattered batch (most of its work in
-// groups whose chunks touch well over the 2 MiB pages their bytes need,
-// group_scattered) to the one-group split shape whole: a quarter of the
-// resident chunks per CU of the fused tail, and the shortest chains.
+// Memory locality: with every lane streaming its own chunk, a load
+// instruction translates 64 addresses, and when the resident chunks lie far
+// apart (a sorted batch whose chunks arrived in random length order) the
+// CU's translation cache (UTCL1) thrashes: 98 % misses instead of ~0 on the
+// same requests, L2 unchanged (tools/tlb_probe.sh, profiles/tlb_r02.json).
+// 65536 x 512 KiB with permuted offsets hashed in 29.2 ms lane-per-chunk
+// against 10.4 in place.  The fused tail's shared loads (8 chunks per
+// instruction, fused_coop_body) take 10.8 ms permuted and 10.7 in place, so
+// the planner ignores layout; the split head still streams lane-per-chunk
+// (one group per CU: 29.3 ms permuted against 24.3 in place), a cost
+// confined to the few longest groups (profiles/mixed_r02.json, "coop").
 constexpr int kSplit8V = kVWK | kVUnmask | kVLayout8 | kVCross;
 constexpr int kMixedThreads = 512;
 
@@ -713,7 +816,7 @@ __global__ __launch_bounds__(kMixedThreads) void sha1_mixed_kernel(BatchArgs A) 
     }
     const uint32_t g = H + (wg - H) * F + wave;
     if (wave >= F || g >= groups) return;
-    fused_body<0>(A, g * 64u + (threadIdx.x & 63u));
+    fused_coop_body<0>(A, g * 64u + (threadIdx.x & 63u), lds + wave * kCoopWaveBytes);
 }
 
 // Makespan model of a sorted ragged batch, microseconds per 64-byte block of
@@ -768,82 +871,14 @@ __device__ double makespan(const uint32_t* sorted_len, uint32_t G, uint32_t C, u
     return m;
 }
 
-// One workgroup.  A scattered batch (see the kernel's comment) gets the
-// all-split plan {0, G, 4}; otherwise every plan is evaluated -- mode 0 with
-// H in [0, hcap] or H = G and F in {4, 8}, and mode 1 -- and the smallest
-// estimate wins (ties: mode 0, smaller H).  forced: write {fmode, fh, ff}
-// as given (tests, A/B).
+// One workgroup.  Every plan is evaluated -- mode 0 with H in [0, hcap] or
+// H = G and F in {4, 8}, and mode 1 -- and the smallest estimate wins (ties:
+// mode 0, smaller H).  The plan depends on the lengths alone: with the fused
+// tail's shared loads, where the chunks lie no longer changes the choice
+// (see the kernel's comment).  forced: write {fmode, fh, ff} as given
+// (tests, A/B).
 constexpr int kPlanThreads = 1024;
 constexpr uint32_t kPlanMaxH = 4096;  // largest split head the model search considers
-
-// Whether group g's chunks are spread over many translation regions: one
-// wave (lane = chunk) counts the distinct 2 MiB pages holding the chunks'
-// first bytes against the fewest pages the group's bytes could fill;
-// scattered above 1.5x that + 1.  Chunks in place in caller order (4 per
-// page at 512 KiB: 16 pages for 16) or in runs sharing pages are not; a
-// longest-first order of chunks that arrived in random length order is (64
-// pages for 1 MiB chunks that would fill 32, for 512 KiB ones 16, for 4 KiB
-// ones 1).  Measured on 65536 x 512 KiB: in place the fused kernel takes
-// 10.6 ms, with the 2 MiB runs scattered 14.8 (still ahead of the split
-// shape's 24.6), with every chunk on a page of its own 29.3 (the split
-// shape: 28.9) -- profiles/mixed_r02.json.
-__device__ __forceinline__ bool group_scattered(uint32_t page, uint32_t kib, bool valid, uint32_t lane) {
-    // lane k's page and size through v_readlane (VALU + scalar adds, no LDS
-    // traffic: the planner is one workgroup on one CU)
-    uint32_t dup = 0, total_kib = 0;
-#pragma unroll
-    for (uint32_t k = 0; k < 64; ++k) {
-        const uint32_t other = __builtin_amdgcn_readlane(page, k);
-        total_kib += __builtin_amdgcn_readlane(kib, k);
-        dup |= (uint32_t)(lane > k) & (uint32_t)(other == page);
-    }
-    const uint32_t distinct = (uint32_t)__popcll(__ballot(valid && !dup));
-    const uint32_t fill = (total_kib + 2047u) / 2048u;  // 2 MiB pages the bytes fill at the least
-    return 2u * distinct > 3u * fill + 2u;
-}
-
-// The scatter test runs on a sample of groups spread evenly over the
-// batch (sample i is group i * G / S, S = min(G, kScatterSample)): the
-// decision is a work-weighted fraction, and the test costs ~200
-// instructions per group on the planner's one CU (every group of a
-// 4096-group batch through LDS shuffles took ~0.8 ms).  One wave takes
-// samples first, first + step, .., their chunk loads kScatterBatch groups at
-// once; returns {work in scattered sampled groups, work in all sampled
-// groups}.
-constexpr uint32_t kScatterBatch = 8, kScatterSample = 256;
-struct FarWork {
-    uint64_t far, all;
-};
-__device__ FarWork scattered_work(const BatchArgs& A, const uint32_t* sorted_len, uint32_t G, uint32_t first,
-                                  uint32_t step, uint32_t lane) {
-    const uint32_t S = min(G, kScatterSample);
-    FarWork w{0, 0};
-    for (uint32_t i0 = first; i0 < S; i0 += kScatterBatch * step) {
-        uint32_t gs[kScatterBatch], id[kScatterBatch], page[kScatterBatch], kib[kScatterBatch];
-        bool valid[kScatterBatch];
-#pragma unroll
-        for (uint32_t j = 0; j < kScatterBatch; ++j) {
-            const uint32_t i = i0 + j * step;
-            gs[j] = i < S ? (uint32_t)((uint64_t)i * G / S) : G;
-            const uint64_t e = 64ull * gs[j] + lane;
-            valid[j] = gs[j] < G && e < A.n;
-            id[j] = valid[j] ? A.order[e] : 0u;
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < kScatterBatch; ++j) {
-            page[j] = valid[j] ? (uint32_t)(A.off[id[j]] >> 21) : 0xffffffffu - lane;
-            kib[j] = valid[j] ? (uint32_t)(((uint64_t)A.len[id[j]] + 1023u) >> 10) : 0u;
-        }
-#pragma unroll
-        for (uint32_t j = 0; j < kScatterBatch; ++j) {
-            if (gs[j] >= G) continue;
-            const uint32_t b = group_blocks(sorted_len, gs[j]);
-            w.all += b;
-            if (group_scattered(page[j], kib[j], valid[j], lane)) w.far += b;
-        }
-    }
-    return w;
-}
 
 __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, const uint32_t* sorted_len,
                                                                   uint32_t cus, uint32_t hcap, int forced,
@@ -868,18 +903,6 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     const uint32_t g0 = min(G, t * per), g1 = min(G, g0 + per);
     uint64_t local = 0;
     for (uint32_t g = g0; g < g1; ++g) local += group_blocks(sorted_len, g);
-    // work in scattered groups (sampled): wave w takes samples w, w + 16, ..
-    __shared__ uint64_t far_sum, sampled_sum;
-    if (t == 0) far_sum = sampled_sum = 0;
-    __syncthreads();
-    {
-        const uint32_t lane = t & 63u, wave = t >> 6, waves = kPlanThreads / 64;
-        const FarWork w = scattered_work(A, sorted_len, G, wave, waves, lane);
-        if (lane == 0 && w.all) {
-            atomicAdd(reinterpret_cast<unsigned long long*>(&far_sum), (unsigned long long)w.far);
-            atomicAdd(reinterpret_cast<unsigned long long*>(&sampled_sum), (unsigned long long)w.all);
-        }
-    }
     scan[t] = local;
     __syncthreads();
     for (uint32_t off = 1; off < kPlanThreads; off <<= 1) {
@@ -889,14 +912,6 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         __syncthreads();
     }
     const uint64_t PG = scan[kPlanThreads - 1];
-    if (2 * far_sum > sampled_sum) {  // scattered: every group in the one-group split shape
-        if (t == 0) {
-            plan[0] = 0;
-            plan[1] = G;
-            plan[2] = 4;
-        }
-        return;
-    }
     // P_H for every candidate H <= hcap, then each thread takes H = t, t + 1024, ..
     uint64_t P = scan[t] - local;  // P_{g0}
     for (uint32_t g = g0; g <= g1 && g <= hcap; ++g) {

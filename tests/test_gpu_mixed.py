@@ -65,31 +65,9 @@ def model_makespan(B, C, mode, H, F, P):
     return m
 
 
-SCATTER_SAMPLE = 256
-
-
-def scattered_work(order, off, lens, B):
-    """plan_mixed_kernel's locality test (group_scattered on the sample
-    scattered_work takes), restated: (work in sampled groups whose chunks
-    start in more distinct 2 MiB pages than 1.5x the pages their bytes fill
-    + 1, work in all sampled groups)."""
-    G = len(B)
-    S = min(G, SCATTER_SAMPLE)
-    far = tot = 0
-    for i in range(S):
-        g = i * G // S
-        ids = order[64 * g:64 * g + 64]
-        pages = np.unique(off[ids].astype(np.uint64) >> np.uint64(21)).size
-        kib = int(((lens[ids].astype(np.int64) + 1023) >> 10).sum())
-        fill = (kib + 2047) // 2048
-        tot += B[g]
-        if 2 * pages > 3 * fill + 2:
-            far += B[g]
-    return far, tot
-
-
-def model_plan(lengths, C, off=None):
-    """plan_mixed_kernel's search, restated: (estimate, mode, H, F)."""
+def model_plan(lengths, C):
+    """plan_mixed_kernel's search, restated: (estimate, mode, H, F).  The
+    lengths alone decide it (not where the chunks lie)."""
     lengths = np.asarray(lengths, np.int64)
     order = np.argsort(-lengths, kind="stable")  # the device's stable radix sort
     srt = lengths[order]
@@ -98,9 +76,6 @@ def model_plan(lengths, C, off=None):
     P = [0]
     for b in B:
         P.append(P[-1] + b)
-    far, tot = scattered_work(order, off, lengths, B) if off is not None else (0, 1)
-    if 2 * far > tot:
-        return (model_makespan(B, C, 0, G, 4, P), 0, G, 4), (B, P)
     hcap, grid = grid_of(G, C)
     best = None
     for H in list(range(hcap + 1)) + ([G] if G > hcap else []):
@@ -210,8 +185,8 @@ def _device_plan(capfd):
 def test_mixed_planner_matches_model(pkg, dev, cus, monkeypatch, capfd, shape):
     """The device planner's plan is the best plan of its model restated here
     (up to ties), on uniform, log-uniform and two-level length mixes, laid
-    out in arrival order (a sorted batch's groups are scattered: all-split
-    plan) and longest-first (contiguous groups: the model's search)."""
+    out in arrival order (each sorted group's chunks far apart) and
+    longest-first (groups contiguous)."""
     torch = dev
     rng = np.random.default_rng(9)
     if shape == "uniform_64k_2.4C":
@@ -236,13 +211,9 @@ def test_mixed_planner_matches_model(pkg, dev, cus, monkeypatch, capfd, shape):
                     torch.from_numpy(lens.astype(np.int32)).cuda(), dig)
     torch.cuda.synchronize()
     mode, H, F = _device_plan(capfd)
-    (best, bmode, bH, bF), (B, P) = model_plan(lens, cus, off)
-    if shape == "mixed_log":  # sorted groups of arrival-order chunks of distinct lengths: scattered
-        assert (bmode, bH, bF) == (0, len(B), 4), shape
-        assert (mode, H, F) == (0, len(B), 4), shape
-    else:
-        got = model_makespan(B, cus, mode, H, F, P)
-        assert got <= best * (1 + 1e-9), (shape, (mode, H, F), got, (bmode, bH, bF), best)
+    (best, bmode, bH, bF), (B, P) = model_plan(lens, cus)
+    got = model_makespan(B, cus, mode, H, F, P)
+    assert got <= best * (1 + 1e-9), (shape, (mode, H, F), got, (bmode, bH, bF), best)
     # every chunk of these batches holds zeros: one digest per distinct length
     d = dig.cpu().numpy()
     for L in rng.choice(np.unique(lens), 12):
