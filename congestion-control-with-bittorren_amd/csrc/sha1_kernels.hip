@@ -152,8 +152,9 @@ __global__ __launch_bounds__(256) void sha1_lane_kernel(BatchArgs A) {
 
 // --------------------------------------------------------------- split ----
 // Workgroup = consumer wave (wave 0) + producer wave (wave 1) on the same 64
-// chunks.  The producer streams each lane's blocks from HBM (per-lane
-// 16-byte loads, two blocks in flight in registers), byte-swaps them and
+// chunks.  The producer streams the wave's blocks from HBM (two blocks or
+// stages in flight in registers; in the product shapes with loads shared
+// across the wave, kVCoop), byte-swaps them and
 // expands the 80-word schedule into an LDS ring; the consumer runs only the
 // 80 rounds, so each chunk's serial instruction stream (the bound when
 // there are too few chunks to fill the SIMDs) drops from ~630 to ~440
@@ -267,6 +268,113 @@ __device__ __forceinline__ void load_stage(const uint8_t* p, Stage& st) {
     }
 }
 
+// ------------------------------------------------------- shared loads ----
+// Bulk loads shared across the wave: instruction i
+// (i = 0..7) of a 128-byte stage reads 128 bytes of each of the group's
+// chunks 8i .. 8i+7 (lane l: chunk 8i + l/8, 16-byte piece l%8), so one load
+// instruction touches 8 chunks instead of 64, and an LDS transpose hands
+// each lane its own chunk's 128 bytes.  The lane-per-chunk pattern makes
+// each load instruction translate 64 addresses; with chunks far apart that
+// thrashes the CU's translation cache: scattered 512 KiB chunks read at
+// 1183 GB/s lane-per-chunk and 5954 GB/s 8 chunks per instruction (5036 /
+// 5980 in place; tools/coop_probe.hip).  In the hash kernels: 65536 x
+// 512 KiB with permuted offsets in 11.1 ms (fused tail) and 24.3 (one-group
+// split) against 28.7 and 29.3 lane-per-chunk; 32768 in the 8-wave split
+// 6.62 ms against 14.8; and in place the split shapes get ~1 % faster
+// (config 2: 6.019 vs 6.067 ms; profiles/mixed_r02.json "coop").
+// Swizzle: piece p of chunk c at c*128 + ((p + c/2) & 7)*16, conflict-free
+// for the b128 stores (8 contiguous lanes write one chunk) and for the b128
+// reads (each of ds_read_b128's 16-lane groups sees 16 distinct 16-byte
+// bank groups).
+constexpr uint32_t kCoopStageBytes = 64u * 128u;
+constexpr uint32_t kCoopWaveBytes = 2u * kCoopStageBytes;
+
+__device__ __forceinline__ uint32_t coop_slot(uint32_t c, uint32_t piece) {
+    return c * 128u + ((piece + (c >> 1)) & 7u) * 16u;
+}
+
+// (the in-flight stage lives in plain 32-bit words: an array of uint4
+// stays in scratch memory)
+__device__ __forceinline__ void coop_load(const uint4* const (&src)[8], uint32_t s, uint32_t (&v)[32]) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const uint4 x = src[i][8u * s];
+        v[4 * i + 0] = x.x;
+        v[4 * i + 1] = x.y;
+        v[4 * i + 2] = x.z;
+        v[4 * i + 3] = x.w;
+    }
+}
+
+__device__ __forceinline__ void coop_store(uint8_t* buf, const uint32_t (&v)[32], uint32_t lane) {
+#pragma unroll
+    for (uint32_t i = 0; i < 8; ++i)
+        *reinterpret_cast<uint4*>(buf + coop_slot(8u * i + lane / 8u, lane & 7u)) =
+            make_uint4(v[4 * i + 0], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+}
+
+__device__ __forceinline__ void coop_read(const uint8_t* buf, uint32_t lane, uint32_t (&w)[32]) {
+#pragma unroll
+    for (uint32_t p = 0; p < 8; ++p) {
+        const uint4 x = *reinterpret_cast<const uint4*>(buf + coop_slot(lane, p));
+        w[4 * p + 0] = x.x;
+        w[4 * p + 1] = x.y;
+        w[4 * p + 2] = x.z;
+        w[4 * p + 3] = x.w;
+    }
+}
+
+
+// The same for one 64-byte block of the wave's 64 chunks (the split
+// producers that own one block per unit): instruction i (i = 0..3) reads
+// block k of chunks 16i .. 16i+15 (lane l: chunk 16i + l/4, 16-byte piece
+// l%4), staged through 4 KiB of LDS.  Piece p of chunk c at
+// c*64 + ((p + c/4) & 3)*16: conflict-free b128 stores and reads, and a
+// lane's store address is the same for every i but for an i*1024 offset.
+__device__ __forceinline__ void coop4_load(const uint4* const (&src)[4], uint32_t k, uint32_t (&v)[16]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const uint4 x = src[i][4u * k];
+        v[4 * i + 0] = x.x;
+        v[4 * i + 1] = x.y;
+        v[4 * i + 2] = x.z;
+        v[4 * i + 3] = x.w;
+    }
+}
+
+__device__ __forceinline__ void coop4_store(uint8_t* buf, const uint32_t (&v)[16], uint32_t lane) {
+    const uint32_t at = (lane >> 2) * 64u + (((lane & 3u) + (lane >> 4)) & 3u) * 16u;
+#pragma unroll
+    for (uint32_t i = 0; i < 4; ++i)
+        *reinterpret_cast<uint4*>(buf + i * 1024u + at) =
+            make_uint4(v[4 * i + 0], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
+}
+
+__device__ __forceinline__ void coop4_read(const uint8_t* buf, uint32_t lane, uint32_t (&w)[16]) {
+#pragma unroll
+    for (uint32_t p = 0; p < 4; ++p) {
+        const uint4 x = *reinterpret_cast<const uint4*>(buf + lane * 64u + ((p + (lane >> 2)) & 3u) * 16u);
+        w[4 * p + 0] = x.x;
+        w[4 * p + 1] = x.y;
+        w[4 * p + 2] = x.z;
+        w[4 * p + 3] = x.w;
+    }
+}
+
+// Per-lane source pointers of the shared-load pattern with `lanes` lanes per
+// chunk: slot i is chunk group*64 + (64/lanes)*i + lane/lanes, piece
+// lane%lanes; a slot past the batch reads the group's first chunk (valid,
+// and at least as long as the wave's bulk region).
+template <int LANES>
+__device__ __forceinline__ void coop_sources(const BatchArgs& A, uint32_t group, uint32_t lane,
+                                             const uint4* (&src)[LANES]) {
+#pragma unroll
+    for (uint32_t i = 0; i < (uint32_t)LANES; ++i) {
+        const uint32_t ej = group * 64u + (64u / LANES) * i + lane / LANES;
+        src[i] = reinterpret_cast<const uint4*>(fetch_entry(A, ej < A.n ? ej : group * 64u).p) + (lane % LANES);
+    }
+}
+
 // Producer side of one bulk stage: blocks 2s, 2s+1 from `cur`; once the
 // second block's words are taken, `cur` is refilled with this producer's
 // stage after next, s + 2 NPROD.
@@ -281,6 +389,43 @@ __device__ __forceinline__ void produce_stage(const Entry& en, uint32_t s, uint3
         if (half == 1 && s + 2 * NPROD < S) load_stage(en.p + 128ull * (s + 2 * NPROD), cur);
         produce_block<U, WK, NPROD>(2 * s + half, w, ring, lane);
     }
+}
+
+// Shared-load producers (kVCoop): the raw 128 bytes (stage) or 64 bytes
+// (own block) of the wave's 64 chunks go through the first bytes of the W
+// slot they are about to fill (free at that point, as for the W writes that
+// follow; the wave's LDS accesses complete in order, so the transposing
+// reads precede the W writes over them).
+template <int U, bool WK, int NPROD = 1>
+__device__ __forceinline__ void produce_stage_coop(const uint4* const (&src)[8], uint32_t s, uint32_t S,
+                                                   uint32_t (&cur)[32], uint8_t* ring, uint32_t lane) {
+    const uint32_t k0 = 2 * s, m = k0 / U, j = k0 - m * U;
+    uint8_t* raw = ring + ((m & 1u) * U + j) * kWBlockBytes;
+    coop_store(raw, cur, lane);
+    if (s + 2 * NPROD < S) coop_load(src, s + 2 * NPROD, cur);
+    uint32_t x[32];
+    coop_read(raw, lane, x);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        uint32_t w[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) w[q] = bswap(x[16 * half + q]);
+        produce_block<U, WK, NPROD>(k0 + half, w, ring, (int)lane);
+    }
+}
+
+template <int U, bool WK, int NPROD>
+__device__ __forceinline__ void produce_own_block_coop(const uint4* const (&src)[4], uint32_t k, uint32_t K,
+                                                       uint32_t (&cur)[16], uint8_t* ring, uint32_t lane) {
+    const uint32_t m = k / U, j = k - m * U;
+    uint8_t* raw = ring + ((m & 1u) * U + j) * kWBlockBytes;
+    coop4_store(raw, cur, lane);
+    if (k + 2 * NPROD < K) coop4_load(src, k + 2 * NPROD, cur);
+    uint32_t w[16];
+    coop4_read(raw, lane, w);
+#pragma unroll
+    for (int q = 0; q < 16; ++q) w[q] = bswap(w[q]);
+    produce_block<U, WK, NPROD>(k, w, ring, (int)lane);
 }
 
 // Producer that owns one block per unit (U == NPROD): block k from `cur`,
@@ -338,6 +483,10 @@ constexpr int kVCross = 256;
 // schedule reads of the next block in one burst before round 0.
 constexpr int kVPrio = 2048;
 constexpr int kVRead20 = 4096;
+// Producers load with shared loads (4 or 8 lanes per chunk, staged through
+// the W slot): one load instruction touches 16 or 8 chunks instead of 64
+// (see `shared loads`).
+constexpr int kVCoop = 8192;
 template <int PAIRS, int V, int NPROD>
 constexpr int kSplitThreads = (V & kVLayout8) ? 512 : 64 * PAIRS * (1 + NPROD) + ((V & kVSkipWave2) ? 64 : 0);
 // Why W+K matters: the consumer's x = e + W + K as a VOP3 v_add3 (K in an
@@ -351,7 +500,7 @@ constexpr int kSplitThreads = (V & kVLayout8) ? 512 : 64 * PAIRS * (1 + NPROD) +
 // 2-block units W+K ~5% ahead, the slot-address form neutral there; unmasked
 // commit helps every shape.
 template <int U>
-constexpr int kSplitV = U == 4 ? (kVWK | kVUnmask | kVSkipWave2 | kVRead10)
+constexpr int kSplitV = U == 4 ? (kVWK | kVUnmask | kVSkipWave2 | kVRead10 | kVCoop)
                                : U == 3 ? (kVRtSlot | kVUnmask) : (kVWK | kVUnmask);
 template <int U>
 constexpr int kSplitNProd = U == 4 ? 2 : 1;
@@ -520,16 +669,31 @@ __device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uin
             // bulk over the full blocks every lane has, then tail/padding
             const uint32_t K = S * 2u;
             uint32_t B0[16], B1[16];
-            if (pidx < K) load_block_a16(en.p + 64ull * pidx, B0);
-            if (pidx + NPROD < K) load_block_a16(en.p + 64ull * (pidx + NPROD), B1);
             uint32_t k = pidx;
-            for (; k + NPROD < K; k += 2 * NPROD) {
-                produce_own_block<U, WK, NPROD>(en, k, K, B0, ring, lane);
-                produce_own_block<U, WK, NPROD>(en, k + NPROD, K, B1, ring, lane);
-            }
-            if (k < K) {
-                produce_own_block<U, WK, NPROD>(en, k, K, B0, ring, lane);
-                k += NPROD;
+            if constexpr ((V & kVCoop) != 0) {
+                const uint4* src[4];
+                coop_sources<4>(A, group, (uint32_t)lane, src);
+                if (pidx < K) coop4_load(src, pidx, B0);
+                if (pidx + NPROD < K) coop4_load(src, pidx + NPROD, B1);
+                for (; k + NPROD < K; k += 2 * NPROD) {
+                    produce_own_block_coop<U, WK, NPROD>(src, k, K, B0, ring, (uint32_t)lane);
+                    produce_own_block_coop<U, WK, NPROD>(src, k + NPROD, K, B1, ring, (uint32_t)lane);
+                }
+                if (k < K) {
+                    produce_own_block_coop<U, WK, NPROD>(src, k, K, B0, ring, (uint32_t)lane);
+                    k += NPROD;
+                }
+            } else {
+                if (pidx < K) load_block_a16(en.p + 64ull * pidx, B0);
+                if (pidx + NPROD < K) load_block_a16(en.p + 64ull * (pidx + NPROD), B1);
+                for (; k + NPROD < K; k += 2 * NPROD) {
+                    produce_own_block<U, WK, NPROD>(en, k, K, B0, ring, lane);
+                    produce_own_block<U, WK, NPROD>(en, k + NPROD, K, B1, ring, lane);
+                }
+                if (k < K) {
+                    produce_own_block<U, WK, NPROD>(en, k, K, B0, ring, lane);
+                    k += NPROD;
+                }
             }
             for (; k < units * U; k += NPROD) {
                 uint32_t w[16];
@@ -540,17 +704,33 @@ __device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uin
             return;
         }
         // this producer's stages: s = pidx, pidx + NPROD, ...
-        Stage A0, A1;
-        if (pidx < S) load_stage(en.p + 128ull * pidx, A0);
-        if (pidx + NPROD < S) load_stage(en.p + 128ull * (pidx + NPROD), A1);
         uint32_t s = pidx;
-        for (; s + NPROD < S; s += 2 * NPROD) {
-            produce_stage<U, WK, NPROD>(en, s, S, A0, ring, lane);
-            produce_stage<U, WK, NPROD>(en, s + NPROD, S, A1, ring, lane);
-        }
-        if (s < S) {
-            produce_stage<U, WK, NPROD>(en, s, S, A0, ring, lane);
-            s += NPROD;
+        if constexpr ((V & kVCoop) != 0) {
+            const uint4* src[8];
+            coop_sources<8>(A, group, (uint32_t)lane, src);
+            uint32_t C0[32], C1[32];
+            if (pidx < S) coop_load(src, pidx, C0);
+            if (pidx + NPROD < S) coop_load(src, pidx + NPROD, C1);
+            for (; s + NPROD < S; s += 2 * NPROD) {
+                produce_stage_coop<U, WK, NPROD>(src, s, S, C0, ring, (uint32_t)lane);
+                produce_stage_coop<U, WK, NPROD>(src, s + NPROD, S, C1, ring, (uint32_t)lane);
+            }
+            if (s < S) {
+                produce_stage_coop<U, WK, NPROD>(src, s, S, C0, ring, (uint32_t)lane);
+                s += NPROD;
+            }
+        } else {
+            Stage A0, A1;
+            if (pidx < S) load_stage(en.p + 128ull * pidx, A0);
+            if (pidx + NPROD < S) load_stage(en.p + 128ull * (pidx + NPROD), A1);
+            for (; s + NPROD < S; s += 2 * NPROD) {
+                produce_stage<U, WK, NPROD>(en, s, S, A0, ring, lane);
+                produce_stage<U, WK, NPROD>(en, s + NPROD, S, A1, ring, lane);
+            }
+            if (s < S) {
+                produce_stage<U, WK, NPROD>(en, s, S, A0, ring, lane);
+                s += NPROD;
+            }
         }
         // tail and padding stages (whole units: blocks past a lane's T are
         // never committed by the consumer)
@@ -654,59 +834,28 @@ __global__ __launch_bounds__(256) void sha1_fused_kernel(BatchArgs A) {
 }
 
 // ---------------------------------------------------------- coop fused ----
-// The fused wave with its bulk loads shared across the wave: instruction i
-// (i = 0..7) of a 128-byte stage reads 128 bytes of each of the group's
-// chunks 8i .. 8i+7 (lane l: chunk 8i + l/8, 16-byte piece l%8), so one load
-// instruction touches 8 chunks instead of 64, and an LDS transpose hands
-// each lane its own chunk's 128 bytes.  The lane-per-chunk pattern makes
-// each load instruction translate 64 addresses; with chunks far apart that
-// thrashes the CU's translation cache: scattered 512 KiB chunks read at
-// 1183 GB/s lane-per-chunk and 5954 GB/s 8 chunks per instruction (5036 /
-// 5980 in place; tools/coop_probe.hip).  Used by the mixed kernel, whose
-// workgroups own the CU's LDS anyway (16 KiB per wave: two stage buffers).
-// Swizzle: piece p of chunk c at c*128 + ((p + c/2) & 7)*16, conflict-free
-// for the b128 stores (8 contiguous lanes write one chunk) and for the b128
-// reads (each of ds_read_b128's 16-lane groups sees 16 distinct 16-byte
-// bank groups).
-constexpr uint32_t kCoopStageBytes = 64u * 128u;
-constexpr uint32_t kCoopWaveBytes = 2u * kCoopStageBytes;
-
-__device__ __forceinline__ uint32_t coop_slot(uint32_t c, uint32_t piece) {
-    return c * 128u + ((piece + (c >> 1)) & 7u) * 16u;
-}
-
-// (the in-flight stage lives in plain 32-bit words: an array of uint4
-// stays in scratch memory)
-__device__ __forceinline__ void coop_load(const uint4* const (&src)[8], uint32_t s, uint32_t (&v)[32]) {
+// The fused wave with its stage loads shared across the wave
+// (coop_load / coop_store / coop_read, above the split kernel).  Used by the
+// mixed kernel, whose workgroups own the CU's LDS anyway (16 KiB per wave:
+// two stage buffers).
+template <int RV>
+__device__ __forceinline__ void coop_compress(const uint32_t (&cur)[32], uint32_t (&h)[5]) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-        const uint4 x = src[i][8u * s];
-        v[4 * i + 0] = x.x;
-        v[4 * i + 1] = x.y;
-        v[4 * i + 2] = x.z;
-        v[4 * i + 3] = x.w;
+    for (int half = 0; half < 2; ++half) {
+        uint32_t w[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = bswap(cur[16 * half + j]);
+        compress<RV>(h, w);
     }
 }
 
-__device__ __forceinline__ void coop_store(uint8_t* buf, const uint32_t (&v)[32], uint32_t lane) {
-#pragma unroll
-    for (uint32_t i = 0; i < 8; ++i)
-        *reinterpret_cast<uint4*>(buf + coop_slot(8u * i + lane / 8u, lane & 7u)) =
-            make_uint4(v[4 * i + 0], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
-}
-
-__device__ __forceinline__ void coop_read(const uint8_t* buf, uint32_t lane, uint32_t (&w)[32]) {
-#pragma unroll
-    for (uint32_t p = 0; p < 8; ++p) {
-        const uint4 x = *reinterpret_cast<const uint4*>(buf + coop_slot(lane, p));
-        w[4 * p + 0] = x.x;
-        w[4 * p + 1] = x.y;
-        w[4 * p + 2] = x.z;
-        w[4 * p + 3] = x.w;
-    }
-}
-
-// lds: this wave's kCoopWaveBytes.  Same contract as fused_body.
+// lds: this wave's kCoopWaveBytes.  Same contract as fused_body.  The
+// wave's LDS accesses complete in order, so a stage's stores precede its
+// reads and the reads of a buffer precede its next stores; hipcc keeps the
+// program order of these lane-dependent accesses it cannot prove disjoint.
+// One stage in flight in registers: a second (as fused_body keeps) was
+// slower -- hipcc moved its loads next to their LDS stores (65536 x 512 KiB
+// 13.1 against 10.4 ms, profiles/coop_split_ab_r02.json).
 template <int RV>
 __device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, uint8_t* lds) {
     const uint32_t group = e / 64u, lane = e & 63u;
@@ -721,14 +870,8 @@ __device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, 
                                  wave_min(valid ? (en.len >> 7) : 0xffffffffu))
                            : 0u;
     if (S > 0) {
-        // this lane's piece of chunks 8i + lane/8; a slot past the batch
-        // reads the group's first chunk (valid, and at least S stages long)
         const uint4* src[8];
-#pragma unroll
-        for (uint32_t i = 0; i < 8; ++i) {
-            const uint32_t ej = group * 64u + 8u * i + lane / 8u;
-            src[i] = reinterpret_cast<const uint4*>(fetch_entry(A, ej < A.n ? ej : group * 64u).p) + (lane & 7u);
-        }
+        coop_sources<8>(A, group, lane, src);
         // stage loads run ahead unconditionally (clamped to the last stage:
         // a repeated read at the end, never past a chunk)
         uint32_t v[32];
@@ -736,21 +879,11 @@ __device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, 
         coop_store(lds, v, lane);
         coop_load(src, min(1u, S - 1u), v);
         for (uint32_t s = 0; s < S; ++s) {
-            // LDS operations of one wave complete in order: this stage's
-            // stores (last iteration) precede these reads, and the next
-            // stage's stores follow them; hipcc keeps the program order of
-            // LDS accesses it cannot prove disjoint (these are lane-dependent).
             uint32_t cur[32];
             coop_read(lds + (s & 1u) * kCoopStageBytes, lane, cur);
             coop_store(lds + ((s + 1u) & 1u) * kCoopStageBytes, v, lane);
             coop_load(src, min(s + 2u, S - 1u), v);
-#pragma unroll
-            for (int half = 0; half < 2; ++half) {
-                uint32_t w[16];
-#pragma unroll
-                for (int j = 0; j < 16; ++j) w[j] = bswap(cur[16 * half + j]);
-                compress<RV>(h, w);
-            }
+            coop_compress<RV>(cur, h);
         }
     }
     if (valid) {
@@ -795,7 +928,7 @@ __device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, 
 // the planner ignores layout; the split head still streams lane-per-chunk
 // (one group per CU: 29.3 ms permuted against 24.3 in place), a cost
 // confined to the few longest groups (profiles/mixed_r02.json, "coop").
-constexpr int kSplit8V = kVWK | kVUnmask | kVLayout8 | kVCross;
+constexpr int kSplit8V = kVWK | kVUnmask | kVLayout8 | kVCross | kVCoop;
 constexpr int kMixedThreads = 512;
 
 __global__ __launch_bounds__(kMixedThreads) void sha1_mixed_kernel(BatchArgs A) {
@@ -1022,7 +1155,7 @@ bool split_unit_built(int u) {
 #ifdef SHA1CHUNK_AB_VARIANTS
     static const int built[] = {1,  2,  3,  4,  8,  9,  10, 11, 12, 20, 21, 22, 23, 24, 26, 27,
                                 30, 31, 32, 33, 34, 36, 37, 42, 44, 45, 46, 504, 505, 506, 507,
-                                569, 577, 578, 579, 580, 581};
+                                569, 577, 578, 579, 580, 581, 13};
     for (int b : built)
         if (u == b) return true;
     return false;
@@ -1090,6 +1223,11 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     case 581:  // 580 + s_setprio 3
         hipLaunchKernelGGL((sha1_split_kernel<4, 1, (77 & ~kVRead10) | kVRead20 | kVPrio, 2>),
                            dim3(groups), dim3(256), 0, st, A);
+        break;
+
+    case 13:  // case 11 with lane-per-chunk producer loads (round-2 A/B of kVCoop)
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, kSplit8V & ~kVCoop, 2>), dim3((groups + 1) / 2), dim3(512), 0,
+                           st, A);
         break;
 
     case 8:  // 4 pairs per workgroup (512 threads), one consumer + producer per SIMD
