@@ -797,6 +797,20 @@ __device__ __forceinline__ void fused_stage(uint32_t s, uint32_t S, const Entry&
     }
 }
 
+// Stages 0 .. S-1 of every lane's chunk, each lane loading its own.
+template <int RV>
+__device__ __forceinline__ void fused_lane_stages(const Entry& en, uint32_t S, uint32_t (&h)[5]) {
+    Stage A0, A1;
+    if (S > 0) load_stage(en.p, A0);
+    if (S > 1) load_stage(en.p + 128, A1);
+    uint32_t s = 0;
+    for (; s + 1 < S; s += 2) {
+        fused_stage<RV>(s, S, en, A0, h);
+        fused_stage<RV>(s + 1, S, en, A1, h);
+    }
+    if (s < S) fused_stage<RV>(s, S, en, A0, h);
+}
+
 // RV: round-sum form (sha1_device.hpp round_step); the product uses 0, the
 // A/B library also builds 1 and 2 (SHA1CHUNK_FUSED_VARIANT).
 // The body of one fused wave: message e's lane (group e / 64).
@@ -813,15 +827,7 @@ __device__ __forceinline__ void fused_body(const BatchArgs& A, uint32_t e) {
                            ? __builtin_amdgcn_readfirstlane(
                                  wave_min(valid ? (en.len >> 7) : 0xffffffffu))
                            : 0u;
-    Stage A0, A1;
-    if (S > 0) load_stage(en.p, A0);
-    if (S > 1) load_stage(en.p + 128, A1);
-    uint32_t s = 0;
-    for (; s + 1 < S; s += 2) {
-        fused_stage<RV>(s, S, en, A0, h);
-        fused_stage<RV>(s + 1, S, en, A1, h);
-    }
-    if (s < S) fused_stage<RV>(s, S, en, A0, h);
+    fused_lane_stages<RV>(en, S, h);
     if (valid) {
         lane_blocks(A, en, 2u * S, h);
         emit(A, en.id, h);
@@ -869,7 +875,23 @@ __device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, 
                            ? __builtin_amdgcn_readfirstlane(
                                  wave_min(valid ? (en.len >> 7) : 0xffffffffu))
                            : 0u;
-    if (S > 0) {
+    // A group whose chunks lie together (in place, or permuted within a
+    // span of about their own bytes) streams lane-per-chunk: no UTCL1
+    // thrash to avoid there, and the shared loads' LDS round trip costs
+    // 1-4 % (profiles/coop_split_ab_r02.json).
+    uint64_t lo = valid ? reinterpret_cast<uint64_t>(en.p) : ~0ull;
+    uint64_t hi = valid ? reinterpret_cast<uint64_t>(en.p) + en.len : 0ull;
+    uint64_t bytes = valid ? en.len : 0ull;
+#pragma unroll
+    for (int m = 32; m >= 1; m >>= 1) {
+        lo = min(lo, (uint64_t)__shfl_xor(lo, m));
+        hi = max(hi, (uint64_t)__shfl_xor(hi, m));
+        bytes += (uint64_t)__shfl_xor(bytes, m);
+    }
+    const bool together = hi - lo <= 2 * bytes + (2ull << 20);
+    if (S > 0 && together) {
+        fused_lane_stages<RV>(en, S, h);
+    } else if (S > 0) {
         const uint4* src[8];
         coop_sources<8>(A, group, lane, src);
         // stage loads run ahead unconditionally (clamped to the last stage:
