@@ -930,8 +930,9 @@ __device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, 
 //           CU in the one-group split shape (4-block units, two producers,
 //           the consumer alone on its SIMD); workgroup H + j hashes groups
 //           H + j*F .. H + j*F + F-1 fused, one group per wave (F = 4: one
-//           wave per SIMD, chain 1.28 us per block; F = 8: two), the stage
-//           loads shared across the wave (fused_coop_body).
+//           wave per SIMD, chain 1.28 us per block; F = 8: two), each
+//           wave loading lane-per-chunk if its chunks lie together and
+//           with loads shared across the wave if not (fused_coop_body).
 //   mode 1: workgroup w hashes groups 2w, 2w+1 in the 8-wave two-pair split
 //           shape (AUTO's shape for C < groups <= 2C on a uniform batch).
 // Blocks in dispatch order: the longest groups start first, and the
@@ -945,11 +946,10 @@ __device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, 
 // CU's translation cache (UTCL1) thrashes: 98 % misses instead of ~0 on the
 // same requests, L2 unchanged (tools/tlb_probe.sh, profiles/tlb_r02.json).
 // 65536 x 512 KiB with permuted offsets hashed in 29.2 ms lane-per-chunk
-// against 10.4 in place.  The fused tail's shared loads (8 chunks per
-// instruction, fused_coop_body) take 10.8 ms permuted and 10.7 in place, so
-// the planner ignores layout; the split head still streams lane-per-chunk
-// (one group per CU: 29.3 ms permuted against 24.3 in place), a cost
-// confined to the few longest groups (profiles/mixed_r02.json, "coop").
+// against 10.4 in place.  Every shape here loads scattered chunks 8 or 16 per
+// instruction (see `shared loads`): permuted, the fused tail takes 10.8 ms
+// and the one-group split shape 24.3 as in place, so the planner ignores
+// layout (profiles/mixed_r02.json, profiles/coop_split_ab_r02.json).
 constexpr int kSplit8V = kVWK | kVUnmask | kVLayout8 | kVCross | kVCoop;
 constexpr int kMixedThreads = 512;
 
