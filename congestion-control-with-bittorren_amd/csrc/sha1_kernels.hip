@@ -1026,6 +1026,55 @@ __device__ double makespan(const uint32_t* sorted_len, uint32_t G, uint32_t C, u
     return m;
 }
 
+// The bounds above are lower bounds: with 160 KiB of LDS per workgroup a CU
+// runs one job at a time, and a long fused job that a CU picks up late ends
+// late (config-5 law at 131072 chunks: bounds 13.0 ms for H = 257, measured
+// 17.4, while H = 160 measured 13.8).  So the planner then simulates the
+// dispatch of a short list of candidate plans exactly and keeps the
+// shortest: workgroup i goes to XCD i % 8 (round-robin), and each XCD starts
+// its jobs in index order on whichever of its CUs frees first.  One lane
+// per (candidate, XCD) keeps its CUs' free times sorted in 32 registers;
+// fp32, restated bit for bit in tests/test_gpu_mixed.py.  Candidates whose
+// bounds already exceed the simulated time of the bounds' best plan are not
+// simulated.
+constexpr uint32_t kSimXcds = 8, kSimCus = 32;      // CUs per XCD the lane tracks at most
+constexpr uint32_t kSimMaxG = 16384;                // groups whose blocks the planner keeps in LDS
+constexpr float kChainSplit4f = 0.742f, kChainFused4f = 1.28f, kChainFused8f = 2.43f,
+                kChainSplit8f = 0.80f;
+
+__device__ __forceinline__ uint32_t plan_jobs(uint32_t G, uint32_t mode, uint32_t H, uint32_t F) {
+    return mode == 1 ? (G + 1u) / 2u : H + (G - H + F - 1u) / F;
+}
+
+__device__ __forceinline__ float sim_job(const uint32_t* blocks, uint32_t mode, uint32_t H, uint32_t F,
+                                         uint32_t j) {
+    if (mode == 1) return (float)blocks[2u * j] * kChainSplit8f;
+    if (j < H) return (float)blocks[j] * kChainSplit4f;
+    return (float)blocks[H + (j - H) * F] * (F == 4 ? kChainFused4f : kChainFused8f);
+}
+
+// Jobs x, x + 8, .. of a plan on one XCD's `per` CUs: the time its last CU
+// frees.  t holds the free times in ascending order (+inf past `per`); a
+// job starts at t[0] and its end is inserted in order.
+__device__ float sim_xcd(const uint32_t* blocks, uint32_t G, uint32_t mode, uint32_t H, uint32_t F,
+                         uint32_t x, uint32_t per) {
+    float t[kSimCus];
+#pragma unroll
+    for (uint32_t i = 0; i < kSimCus; ++i) t[i] = i < per ? 0.0f : __builtin_inff();
+    const uint32_t J = plan_jobs(G, mode, H, F);
+    for (uint32_t j = x; j < J; j += kSimXcds) {
+        const float nx = t[0] + sim_job(blocks, mode, H, F, j);
+#pragma unroll
+        for (uint32_t i = 0; i + 1 < kSimCus; ++i) t[i] = t[i + 1] <= nx ? t[i + 1] : fmaxf(t[i], nx);
+        t[kSimCus - 1] = fmaxf(t[kSimCus - 1], nx);
+    }
+    float last = 0.0f;
+#pragma unroll
+    for (uint32_t i = 0; i < kSimCus; ++i)
+        if (i < per) last = fmaxf(last, t[i]);
+    return last;
+}
+
 // One workgroup.  Every plan is evaluated -- mode 0 with H in [0, hcap] or
 // H = G and F in {4, 8}, and mode 1 -- and the smallest estimate wins (ties:
 // mode 0, smaller H).  The plan depends on the lengths alone: with the fused
@@ -1057,7 +1106,12 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     const uint32_t per = (G + kPlanThreads - 1) / kPlanThreads;
     const uint32_t g0 = min(G, t * per), g1 = min(G, g0 + per);
     uint64_t local = 0;
-    for (uint32_t g = g0; g < g1; ++g) local += group_blocks(sorted_len, g);
+    __shared__ uint32_t blocks[kSimMaxG];  // group_blocks of groups < kSimMaxG, for the simulation
+    for (uint32_t g = g0; g < g1; ++g) {
+        const uint32_t b = group_blocks(sorted_len, g);
+        if (g < kSimMaxG) blocks[g] = b;
+        local += b;
+    }
     scan[t] = local;
     __syncthreads();
     for (uint32_t off = 1; off < kPlanThreads; off <<= 1) {
@@ -1102,11 +1156,72 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         }
         __syncthreads();
     }
+    const bool simulate = G <= kSimMaxG && cus % kSimXcds == 0 && cus / kSimXcds <= kSimCus;
+    if (!simulate) {
+        if (t == 0) {
+            const bool split8 = makespan(sorted_len, G, cus, 1, 0, 0, 0, PG) < best_m[0];
+            plan[0] = split8 ? 1u : 0u;
+            plan[1] = split8 ? 0u : best_h[0];
+            plan[2] = split8 ? 0u : best_f[0];
+        }
+        return;
+    }
+    // Candidates: the bounds' best plan, the 8-wave mode, all-split, split
+    // heads around the bounds' best, and a grid of heads up to 2C (both F).
+    constexpr uint32_t kMaxCand = kPlanThreads / kSimXcds;
+    __shared__ uint32_t cmode[kMaxCand], chead[kMaxCand], cf[kMaxCand], ncand;
+    __shared__ float cmk[kMaxCand];
     if (t == 0) {
-        const bool split8 = makespan(sorted_len, G, cus, 1, 0, 0, 0, PG) < best_m[0];
-        plan[0] = split8 ? 1u : 0u;
-        plan[1] = split8 ? 0u : best_h[0];
-        plan[2] = split8 ? 0u : best_f[0];
+        uint32_t k = 0;
+        auto add = [&](uint32_t m, uint32_t h, uint32_t f) {
+            cmode[k] = m;
+            chead[k] = h;
+            cf[k] = h == G ? 4u : f;
+            ++k;
+        };
+        const uint32_t hb = best_h[0], fb = best_f[0];
+        add(0, hb, fb);
+        add(1, 0, 0);
+        add(0, G, 4);
+        for (uint32_t d = 1; d <= 64; d *= 2) {
+            if (hb >= d) add(0, hb - d, fb);
+            if (hb + d <= hcap) add(0, hb + d, fb);
+        }
+        const uint32_t top = min(hcap, 2u * cus);
+        for (uint32_t i = 0; i < 32; ++i) {
+            const uint32_t h = i * top / 31u;
+            add(0, h, 4);
+            if (h < G) add(0, h, 8);
+        }
+        ncand = k;
+    }
+    __syncthreads();
+    // Pass 1 simulates the bounds' plan; pass 2 every other candidate whose
+    // bounds are below that time (the rest cannot beat it; a 4096-group
+    // all-split candidate alone is ~100 us of simulation).
+    const uint32_t c = t / kSimXcds, x = t % kSimXcds;
+    for (uint32_t pass = 0; pass < 2; ++pass) {
+        bool run = pass == 0 ? c == 0 : (c >= 1 && c < ncand);
+        if (run && pass == 1) {
+            const uint32_t m = cmode[c], h = chead[c], f = cf[c];
+            const double lb = m == 1 ? makespan(sorted_len, G, cus, 1, 0, 0, 0, PG)
+                                     : makespan(sorted_len, G, cus, 0, h, f, h <= hcap ? prefix[h] : PG, PG);
+            run = lb < (double)cmk[0];
+        }
+        float mk = __builtin_inff();
+        if (run) mk = sim_xcd(blocks, G, cmode[c], chead[c], cf[c], x, cus / kSimXcds);
+#pragma unroll
+        for (uint32_t m = 1; m < kSimXcds; m *= 2) mk = fmaxf(mk, __shfl_xor(mk, m));
+        if (x == 0 && (pass == 0 ? c == 0 : c >= 1)) cmk[c] = mk;
+        __syncthreads();
+    }
+    if (t == 0) {
+        uint32_t bi = 0;
+        for (uint32_t i = 1; i < ncand; ++i)
+            if (cmk[i] < cmk[bi]) bi = i;
+        plan[0] = cmode[bi];
+        plan[1] = cmode[bi] == 1 ? 0u : chead[bi];
+        plan[2] = cmode[bi] == 1 ? 0u : cf[bi];
     }
 }
 

@@ -65,9 +65,63 @@ def model_makespan(B, C, mode, H, F, P):
     return m
 
 
-def model_plan(lengths, C):
+CHAIN32 = {k: np.float32(v) for k, v in CHAIN.items()}
+SIM_XCDS, SIM_CUS, SIM_MAX_G = 8, 32, 16384
+
+
+def sim_xcd(B, mode, H, F, x, per):
+    """plan_mixed_kernel's sim_xcd in the same fp32 operations: XCD x's jobs
+    (x, x + 8, ..) started in order on whichever of its `per` CUs frees
+    first; the time the last one frees."""
+    G = len(B)
+    J = (G + 1) // 2 if mode == 1 else H + (G - H + F - 1) // F
+    t = np.zeros(per, np.float32)  # ascending
+    for j in range(x, J, SIM_XCDS):
+        if mode == 1:
+            p = np.float32(B[2 * j]) * CHAIN32["split8"]
+        elif j < H:
+            p = np.float32(B[j]) * CHAIN32["split4"]
+        else:
+            p = np.float32(B[H + (j - H) * F]) * CHAIN32[f"fused{F}"]
+        nx = np.float32(t[0] + p)
+        t = np.sort(np.append(t[1:], nx))
+    return np.float32(t[-1]) if per else np.float32(0)
+
+
+def sim_plan(B, C, mode, H, F):
+    return max(sim_xcd(B, mode, H, F, x, C // SIM_XCDS) for x in range(SIM_XCDS))
+
+
+def candidates(G, C, hcap, hb, fb):
+    """plan_mixed_kernel's candidate list, in its order."""
+    out = []
+
+    def add(m, h, f):
+        out.append((m, h, 4 if h == G else f))
+    add(0, hb, fb)
+    add(1, 0, 0)
+    add(0, G, 4)
+    d = 1
+    while d <= 64:
+        if hb >= d:
+            add(0, hb - d, fb)
+        if hb + d <= hcap:
+            add(0, hb + d, fb)
+        d *= 2
+    top = min(hcap, 2 * C)
+    for i in range(32):
+        h = i * top // 31
+        add(0, h, 4)
+        if h < G:
+            add(0, h, 8)
+    return out
+
+
+def model_plan(lengths, C, simulate=True):
     """plan_mixed_kernel's search, restated: (estimate, mode, H, F).  The
-    lengths alone decide it (not where the chunks lie)."""
+    lengths alone decide it (not where the chunks lie).  Stage 1 minimises
+    the makespan bounds; stage 2 simulates the dispatch of the candidate
+    plans and keeps the first shortest (estimate: its simulated time)."""
     lengths = np.asarray(lengths, np.int64)
     order = np.argsort(-lengths, kind="stable")  # the device's stable radix sort
     srt = lengths[order]
@@ -83,10 +137,20 @@ def model_plan(lengths, C):
             m = model_makespan(B, C, 0, H, F, P)
             if best is None or m < best[0]:
                 best = (m, 0, H, F)
-    m = model_makespan(B, C, 1, 0, 0, P)
-    if m < best[0]:
-        best = (m, 1, 0, 0)
-    return best, (B, P)
+    if not (simulate and G <= SIM_MAX_G and C % SIM_XCDS == 0 and C // SIM_XCDS <= SIM_CUS):
+        m = model_makespan(B, C, 1, 0, 0, P)
+        if m < best[0]:
+            best = (m, 1, 0, 0)
+        return best, (B, P)
+    cands = candidates(G, C, hcap, best[2], best[3])
+    s0 = sim_plan(B, C, *cands[0])
+    sims = [(s0,) + cands[0]]
+    for m, h, f in cands[1:]:  # pass 2: only candidates whose bounds are below s0
+        lb = model_makespan(B, C, m, h, f, P)
+        sims.append((sim_plan(B, C, m, h, f) if lb < float(s0) else np.float32(np.inf), m, h, f))
+    i = min(range(len(sims)), key=lambda k: (sims[k][0], k))
+    mk, m, h, f = sims[i]
+    return (float(mk), m, 0 if m == 1 else h, 0 if m == 1 else f), (B, P)
 
 
 def ragged(rng, n, long_n, long_lo, long_hi, short_hi, aligned=True):
@@ -184,7 +248,7 @@ def _device_plan(capfd):
                                    "two_level", "two_level_sorted"])
 def test_mixed_planner_matches_model(pkg, dev, cus, monkeypatch, capfd, shape):
     """The device planner's plan is the best plan of its model restated here
-    (up to ties), on uniform, log-uniform and two-level length mixes, laid
+    (up to ties: bounds, then the simulated dispatch of the candidates), on uniform, log-uniform and two-level length mixes, laid
     out in arrival order (each sorted group's chunks far apart) and
     longest-first (groups contiguous)."""
     torch = dev
@@ -212,8 +276,9 @@ def test_mixed_planner_matches_model(pkg, dev, cus, monkeypatch, capfd, shape):
     torch.cuda.synchronize()
     mode, H, F = _device_plan(capfd)
     (best, bmode, bH, bF), (B, P) = model_plan(lens, cus)
-    got = model_makespan(B, cus, mode, H, F, P)
-    assert got <= best * (1 + 1e-9), (shape, (mode, H, F), got, (bmode, bH, bF), best)
+    simulated = len(B) <= SIM_MAX_G and cus % SIM_XCDS == 0 and cus // SIM_XCDS <= SIM_CUS
+    got = float(sim_plan(B, cus, mode, H, F)) if simulated else model_makespan(B, cus, mode, H, F, P)
+    assert got <= best * (1 + 1e-6), (shape, (mode, H, F), got, (bmode, bH, bF), best)
     # every chunk of these batches holds zeros: one digest per distinct length
     d = dig.cpu().numpy()
     for L in rng.choice(np.unique(lens), 12):
