@@ -993,11 +993,18 @@ __device__ __forceinline__ uint32_t group_blocks(const uint32_t* sorted_len, uin
 // The workgroups of a plan are jobs that the dispatcher starts in index
 // order on whichever CU frees first.  Job i of mode 0 (H split groups, then
 // fused workgroups of F groups) and of mode 1 (pairs): its duration.
-__device__ __forceinline__ double job_time(const uint32_t* sorted_len, uint32_t mode, uint32_t H,
-                                           uint32_t F, uint32_t i) {
-    if (mode == 1) return group_blocks(sorted_len, 2u * i) * kChainSplit8;
-    if (i < H) return group_blocks(sorted_len, i) * kChainSplit4;
-    return group_blocks(sorted_len, H + (i - H) * F) * (F == 4 ? kChainFused4 : kChainFused8);
+// (blocks: the planner's LDS copy of group_blocks for groups < kSimMaxG)
+constexpr uint32_t kSimMaxG = 16384;  // groups whose blocks the planner keeps in LDS
+
+__device__ __forceinline__ uint32_t plan_blocks(const uint32_t* sorted_len, const uint32_t* blocks, uint32_t g) {
+    return g < kSimMaxG ? blocks[g] : group_blocks(sorted_len, g);
+}
+
+__device__ __forceinline__ double job_time(const uint32_t* sorted_len, const uint32_t* blocks, uint32_t mode,
+                                           uint32_t H, uint32_t F, uint32_t i) {
+    if (mode == 1) return plan_blocks(sorted_len, blocks, 2u * i) * kChainSplit8;
+    if (i < H) return plan_blocks(sorted_len, blocks, i) * kChainSplit4;
+    return plan_blocks(sorted_len, blocks, H + (i - H) * F) * (F == 4 ? kChainFused4 : kChainFused8);
 }
 
 // Estimated makespan of a plan: the largest of
@@ -1008,8 +1015,8 @@ __device__ __forceinline__ double job_time(const uint32_t* sorted_len, uint32_t 
 //                                 for equal lengths)
 // where W = cu_split4 * P_H + cu_fusedF * (P_G - P_H) in mode 0 and
 // cu_split8 * P_G in mode 1 (P_H: blocks of groups 0 .. H-1).
-__device__ double makespan(const uint32_t* sorted_len, uint32_t G, uint32_t C, uint32_t mode, uint32_t H,
-                           uint32_t F, uint64_t PH, uint64_t PG) {
+__device__ double makespan(const uint32_t* sorted_len, const uint32_t* blocks, uint32_t G, uint32_t C,
+                           uint32_t mode, uint32_t H, uint32_t F, uint64_t PH, uint64_t PG) {
     double W;
     uint32_t J;
     if (mode == 1) {
@@ -1019,10 +1026,10 @@ __device__ double makespan(const uint32_t* sorted_len, uint32_t G, uint32_t C, u
         W = kCuSplit4 * (double)PH + (F == 4 ? kCuFused4 : kCuFused8) * (double)(PG - PH);
         J = H + (G - H + F - 1u) / F;
     }
-    double m = fmax(W / C, job_time(sorted_len, mode, H, F, 0));
-    if (mode == 0 && H > 0 && H < G) m = fmax(m, job_time(sorted_len, mode, H, F, H));
+    double m = fmax(W / C, job_time(sorted_len, blocks, mode, H, F, 0));
+    if (mode == 0 && H > 0 && H < G) m = fmax(m, job_time(sorted_len, blocks, mode, H, F, H));
     for (uint32_t k = 1; (uint64_t)k * C < J; ++k)
-        m = fmax(m, (k + 1) * job_time(sorted_len, mode, H, F, k * C));
+        m = fmax(m, (k + 1) * job_time(sorted_len, blocks, mode, H, F, k * C));
     return m;
 }
 
@@ -1038,7 +1045,6 @@ __device__ double makespan(const uint32_t* sorted_len, uint32_t G, uint32_t C, u
 // bounds already exceed the simulated time of the bounds' best plan are not
 // simulated.
 constexpr uint32_t kSimXcds = 8, kSimCus = 32;      // CUs per XCD the lane tracks at most
-constexpr uint32_t kSimMaxG = 16384;                // groups whose blocks the planner keeps in LDS
 constexpr float kChainSplit4f = 0.742f, kChainFused4f = 1.28f, kChainFused8f = 2.43f,
                 kChainSplit8f = 0.80f;
 
@@ -1062,10 +1068,12 @@ __device__ float sim_xcd(const uint32_t* blocks, uint32_t G, uint32_t mode, uint
 #pragma unroll
     for (uint32_t i = 0; i < kSimCus; ++i) t[i] = i < per ? 0.0f : __builtin_inff();
     const uint32_t J = plan_jobs(G, mode, H, F);
+#pragma unroll 4
     for (uint32_t j = x; j < J; j += kSimXcds) {
         const float nx = t[0] + sim_job(blocks, mode, H, F, j);
+        // t ascending: the new t[i] is nx clamped to [t[i], t[i+1]]
 #pragma unroll
-        for (uint32_t i = 0; i + 1 < kSimCus; ++i) t[i] = t[i + 1] <= nx ? t[i + 1] : fmaxf(t[i], nx);
+        for (uint32_t i = 0; i + 1 < kSimCus; ++i) t[i] = __builtin_amdgcn_fmed3f(t[i], nx, t[i + 1]);
         t[kSimCus - 1] = fmaxf(t[kSimCus - 1], nx);
     }
     float last = 0.0f;
@@ -1125,19 +1133,19 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     uint64_t P = scan[t] - local;  // P_{g0}
     for (uint32_t g = g0; g <= g1 && g <= hcap; ++g) {
         prefix[g] = P;
-        if (g < g1) P += group_blocks(sorted_len, g);
+        if (g < g1) P += plan_blocks(sorted_len, blocks, g);
     }
     __syncthreads();
     double bm = 1e300;
     uint32_t bh = 0, bf = 4;
     for (uint32_t H = t; H <= hcap; H += kPlanThreads) {
         for (uint32_t F = 4; F <= (H < G ? 8u : 4u); F += 4) {  // H = G: every group split
-            const double m = makespan(sorted_len, G, cus, 0, H, F, prefix[H], PG);
+            const double m = makespan(sorted_len, blocks, G, cus, 0, H, F, prefix[H], PG);
             if (m < bm) { bm = m; bh = H; bf = F; }
         }
     }
     if (t == 0 && G > hcap) {  // H = G beyond the searched head sizes
-        const double m = makespan(sorted_len, G, cus, 0, G, 4, PG, PG);
+        const double m = makespan(sorted_len, blocks, G, cus, 0, G, 4, PG, PG);
         if (m < bm) { bm = m; bh = G; bf = 4; }
     }
     best_m[t] = bm;
@@ -1159,7 +1167,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     const bool simulate = G <= kSimMaxG && cus % kSimXcds == 0 && cus / kSimXcds <= kSimCus;
     if (!simulate) {
         if (t == 0) {
-            const bool split8 = makespan(sorted_len, G, cus, 1, 0, 0, 0, PG) < best_m[0];
+            const bool split8 = makespan(sorted_len, blocks, G, cus, 1, 0, 0, 0, PG) < best_m[0];
             plan[0] = split8 ? 1u : 0u;
             plan[1] = split8 ? 0u : best_h[0];
             plan[2] = split8 ? 0u : best_f[0];
@@ -1204,8 +1212,8 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         bool run = pass == 0 ? c == 0 : (c >= 1 && c < ncand);
         if (run && pass == 1) {
             const uint32_t m = cmode[c], h = chead[c], f = cf[c];
-            const double lb = m == 1 ? makespan(sorted_len, G, cus, 1, 0, 0, 0, PG)
-                                     : makespan(sorted_len, G, cus, 0, h, f, h <= hcap ? prefix[h] : PG, PG);
+            const double lb = m == 1 ? makespan(sorted_len, blocks, G, cus, 1, 0, 0, 0, PG)
+                                     : makespan(sorted_len, blocks, G, cus, 0, h, f, h <= hcap ? prefix[h] : PG, PG);
             run = lb < (double)cmk[0];
         }
         float mk = __builtin_inff();
