@@ -1227,6 +1227,11 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         uint32_t bi = 0;
         for (uint32_t i = 1; i < ncand; ++i)
             if (cmk[i] < cmk[bi]) bi = i;
+        // All-split (candidate 2) within 0.5 % of the best is taken instead:
+        // a chain-bound batch then runs with no fused waves heating the chip
+        // (65536 chunks of the config-5 law: 12.14 ms all-split against 12.50
+        // for a split head + fused tail simulated as equal).
+        if (cmk[2] <= cmk[bi] * 1.005f) bi = 2;
         plan[0] = cmode[bi];
         plan[1] = cmode[bi] == 1 ? 0u : chead[bi];
         plan[2] = cmode[bi] == 1 ? 0u : cf[bi];

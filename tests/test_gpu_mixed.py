@@ -149,6 +149,8 @@ def model_plan(lengths, C, simulate=True):
         lb = model_makespan(B, C, m, h, f, P)
         sims.append((sim_plan(B, C, m, h, f) if lb < float(s0) else np.float32(np.inf), m, h, f))
     i = min(range(len(sims)), key=lambda k: (sims[k][0], k))
+    if sims[2][0] <= np.float32(sims[i][0]) * np.float32(1.005):  # all-split near the best: taken
+        i = 2
     mk, m, h, f = sims[i]
     return (float(mk), m, 0 if m == 1 else h, 0 if m == 1 else f), (B, P)
 
