@@ -288,6 +288,28 @@ def test_mixed_planner_matches_model(pkg, dev, cus, monkeypatch, capfd, shape):
         assert d[i].tobytes() == hashlib.sha1(bytes(int(L))).digest()
 
 
+def test_mixed_beyond_simulated_group_count(pkg, dev, oracle, cus, monkeypatch, capfd):
+    """More groups than the planner keeps in LDS (SIM_MAX_G = 16384): the
+    bounds-only plan, a grid of G workgroups, every digest against the
+    oracle.  1.05 M short chunks (0 .. 300 bytes, a few of 40 KiB)."""
+    torch = dev
+    rng = np.random.default_rng(16385)
+    G = SIM_MAX_G + 3
+    n = 64 * G - 17
+    lens = rng.integers(0, 300, n).astype(np.uint32)
+    lens[rng.choice(n, 2000, replace=False)] = rng.integers(30000, 40000, 2000)
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum((lens.astype(np.uint64) + 15) // 16 * 16)[: n - 1]
+    host = rng.integers(0, 256, int(off[-1] + lens[-1]) + 64, dtype=np.uint8)
+    want = oracle.hash_batch(host, off, lens)
+    got = run(pkg, torch, host, off, lens, {"SHA1CHUNK_MIXED_DEBUG": "1"}, monkeypatch)
+    _check(got, want, "bounds-only plan")
+    mode, H, F = _device_plan(capfd)
+    (best, bmode, bH, bF), (B, P) = model_plan(lens, cus)
+    assert len(B) > SIM_MAX_G
+    assert model_makespan(B, cus, mode, H, F, P) <= best * (1 + 1e-9), ((mode, H, F), (bmode, bH, bF))
+
+
 def test_mixed_config5_law_at_4x(pkg, dev, oracle, cus, monkeypatch):
     """BASELINE config 5's length law (4 KiB .. 1 MiB, ragged tails) at 65536
     chunks (12 GiB resident, 4 groups per CU): AUTO's mixed kernel against
