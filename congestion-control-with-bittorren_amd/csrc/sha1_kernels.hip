@@ -1083,12 +1083,14 @@ __device__ float sim_xcd(const uint32_t* blocks, uint32_t G, uint32_t mode, uint
     return last;
 }
 
-// One workgroup.  Every plan is evaluated -- mode 0 with H in [0, hcap] or
-// H = G and F in {4, 8}, and mode 1 -- and the smallest estimate wins (ties:
-// mode 0, smaller H).  The plan depends on the lengths alone: with the fused
-// tail's shared loads, where the chunks lie no longer changes the choice
-// (see the kernel's comment).  forced: write {fmode, fh, ff} as given
-// (tests, A/B).
+// One workgroup, two stages.  Bounds: every mode-0 plan (H in [0, hcap] or
+// H = G, F in {4, 8}) gets the makespan bounds above, the smallest wins
+// (ties: smaller H).  Simulation (up to kSimMaxG groups on 8 XCDs of <= 32
+// CUs): ~80 candidates around it are simulated and the shortest wins, or
+// all-split within 0.5 % of it; beyond that, the bounds' plan or mode 1 by
+// the same bounds.  The plan depends on the lengths alone: with shared
+// loads where the chunks lie no longer changes the choice (see the
+// kernel's comment).  forced: write {fmode, fh, ff} as given (tests, A/B).
 constexpr int kPlanThreads = 1024;
 constexpr uint32_t kPlanMaxH = 4096;  // largest split head the model search considers
 
