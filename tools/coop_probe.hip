@@ -11,7 +11,8 @@
 //           chunks (8 chunks per instruction)
 //   coop64  64 lanes per chunk: one instruction reads 1 KiB of one chunk
 //
-// Every wave owns 64 chunks and every pattern reads the same bytes; 256
+// Layouts: in place, permuted at random, and permuted in runs of 4
+// adjacent chunks.  Every wave owns 64 chunks and every pattern reads the same bytes; 256
 // threads per workgroup, N / 256 workgroups (N = 65536: one per CU, four
 // waves = 256 resident chunks per CU, the fused kernel's F = 4 shape).
 // XOR/add-folded into one dword per lane so nothing is dead.
@@ -116,10 +117,16 @@ int main(int argc, char** argv) {
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
-    for (int layout = 0; layout < 2; ++layout) {
+    for (int layout = 0; layout < 3; ++layout) {
         std::vector<uint32_t> perm(N);
         for (uint32_t i = 0; i < N; ++i) perm[i] = i;
-        if (layout) std::shuffle(perm.begin(), perm.end(), std::mt19937(1));
+        if (layout == 1) std::shuffle(perm.begin(), perm.end(), std::mt19937(1));
+        if (layout == 2) {  // runs of 4 adjacent chunks, the runs permuted
+            std::vector<uint32_t> runs(N / 4);
+            for (uint32_t r = 0; r < N / 4; ++r) runs[r] = r;
+            std::shuffle(runs.begin(), runs.end(), std::mt19937(1));
+            for (uint32_t i = 0; i < N; ++i) perm[i] = runs[i / 4] * 4 + i % 4;
+        }
         for (uint32_t i = 0; i < N; ++i) off[i] = (uint64_t)perm[i] * L;
         CHECK(hipMemcpy(d_off, off.data(), N * sizeof(uint64_t), hipMemcpyHostToDevice));
         for (int pat = 0; pat < 3; ++pat) {
@@ -139,7 +146,7 @@ int main(int argc, char** argv) {
             static const char* names[] = {"lane", "coop8", "coop64"};
             printf("{\"layout\": \"%s\", \"pattern\": \"%s\", \"chunks\": %u, \"chunk_bytes\": %u, \"ms\": %.3f, "
                    "\"GBps\": %.1f}\n",
-                   layout ? "scattered" : "in_place", names[pat], N, L, best, (double)N * L / (best * 1e-3) / 1e9);
+                   layout == 1 ? "scattered" : layout == 2 ? "runs_of_4" : "in_place", names[pat], N, L, best, (double)N * L / (best * 1e-3) / 1e9);
             fflush(stdout);
         }
     }
