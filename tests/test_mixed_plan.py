@@ -121,3 +121,21 @@ def test_plan_ignores_arrival_order():
     assert M.model_plan(lens, C)[0] == M.model_plan(np.sort(lens)[::-1].copy(), C)[0]
     rng = np.random.default_rng(3)
     assert M.model_plan(lens, C)[0] == M.model_plan(rng.permutation(lens), C)[0]
+
+
+@pytest.mark.parametrize("G", [257, 300, 511, 512, 513, 1024, 1025, 4096, 16384])
+def test_candidates_are_valid_plans(G):
+    """Every candidate the planner simulates is a plan the mixed kernel runs
+    (H <= hcap or H = G, F in {4, 8}, F = 4 when H = G) and they fit its
+    128 simulation slots; the bounds' plan is candidate 0, all-split 2."""
+    hcap, _ = M.grid_of(G, C)
+    for hb in (0, 1, hcap // 2, hcap):
+        for fb in (4, 8):
+            cands = M.candidates(G, C, hcap, hb, fb)
+            assert len(cands) <= 128
+            assert cands[0] == (0, hb, 4 if hb == G else fb) and cands[1] == (1, 0, 0) and cands[2] == (0, G, 4)
+            for m, h, f in cands:
+                if m == 1:
+                    continue
+                assert h <= hcap or h == G, (h, hcap, G)
+                assert f in (4, 8) and (h < G or f == 4)
