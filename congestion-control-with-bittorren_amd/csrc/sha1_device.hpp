@@ -201,6 +201,31 @@ __device__ __forceinline__ void load_block_any(const uint8_t* p, uint32_t (&w)[1
     for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
 }
 
+// K dwords from any byte alignment, loaded raw now and shifted at use (so a
+// prefetch does not wait for its loads): d holds the K + 1 dwords from
+// p & ~3 (the last only when p is not 4-byte aligned; it then holds at
+// least one byte of the span, so it never crosses into another page), and
+// word j is alignbyte(d[j+1], d[j], p & 3).
+template <int K>
+struct RawSpan {
+    uint32_t d[K + 1];
+};
+
+template <int K>
+__device__ __forceinline__ void load_raw(const uint8_t* p, RawSpan<K>& r) {
+    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+#pragma unroll
+    for (int j = 0; j < K; ++j) r.d[j] = q[j];
+    r.d[K] = (a & 3u) ? q[K] : 0u;
+}
+
+template <int K, int J0 = 0, int N = K>
+__device__ __forceinline__ void shift_raw(const RawSpan<K>& r, uint32_t sh, uint32_t (&w)[N]) {
+#pragma unroll
+    for (int j = 0; j < N; ++j) w[j] = __builtin_amdgcn_alignbyte(r.d[J0 + j + 1], r.d[J0 + j], sh);
+}
+
 __device__ __forceinline__ void load_block_partial(const uint8_t* p, uint32_t avail,
                                                    uint32_t (&w)[16]) {
     const uintptr_t a = reinterpret_cast<uintptr_t>(p);

@@ -137,6 +137,11 @@ __device__ __forceinline__ uint32_t wave_max(uint32_t x) {
     return x;
 }
 
+// Bulk stages every lane has: the wave's fewest whole 128-byte stages.
+__device__ __forceinline__ uint32_t bulk_stages(const Entry& en, bool valid) {
+    return wave_any(valid) ? __builtin_amdgcn_readfirstlane(wave_min(valid ? (en.len >> 7) : 0xffffffffu)) : 0u;
+}
+
 }  // namespace
 
 // ---------------------------------------------------------------- lane ----
@@ -428,6 +433,37 @@ __device__ __forceinline__ void produce_own_block_coop(const uint4* const (&src)
     produce_block<U, WK, NPROD>(k, w, ring, (int)lane);
 }
 
+// The same two producers for a wave whose chunks are not all 16-byte
+// aligned: loads of any alignment (RawSpan: dwords from p & ~3, shifted by
+// p & 3 at use), with the same registers-ahead prefetch.
+template <int U, bool WK, int NPROD = 1>
+__device__ __forceinline__ void produce_stage_any(const Entry& en, uint32_t s, uint32_t S, RawSpan<32>& cur,
+                                                  uint8_t* ring, int lane) {
+    const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(en.p) & 3u);
+    uint32_t w[16];
+    shift_raw<32, 0, 16>(cur, sh, w);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
+    produce_block<U, WK, NPROD>(2 * s, w, ring, lane);
+    shift_raw<32, 16, 16>(cur, sh, w);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
+    if (s + 2 * NPROD < S) load_raw<32>(en.p + 128ull * (s + 2 * NPROD), cur);
+    produce_block<U, WK, NPROD>(2 * s + 1, w, ring, lane);
+}
+
+template <int U, bool WK, int NPROD>
+__device__ __forceinline__ void produce_own_block_any(const Entry& en, uint32_t k, uint32_t K, RawSpan<16>& cur,
+                                                      uint8_t* ring, int lane) {
+    const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(en.p) & 3u);
+    uint32_t w[16];
+    shift_raw<16>(cur, sh, w);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
+    if (k + 2 * NPROD < K) load_raw<16>(en.p + 64ull * (k + 2 * NPROD), cur);
+    produce_block<U, WK, NPROD>(k, w, ring, lane);
+}
+
 // Producer that owns one block per unit (U == NPROD): block k from `cur`,
 // which is then refilled with this producer's block after next, k + 2 NPROD.
 template <int U, bool WK, int NPROD>
@@ -656,21 +692,32 @@ __device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uin
 
     if (producer) {
         // ----------------------------- producer -------------------------
-        // Bulk: stages (2 full blocks) that every lane has, when every lane's
-        // chunk is 16-byte aligned (branch-free loads hipcc can count);
+        // Bulk: stages (2 full blocks) that every lane has, with
+        // branch-free loads hipcc can count (16-byte ones when every lane's
+        // chunk is 16-byte aligned, dword + funnel-shift ones otherwise);
         // registers hold the current stage and the next one in flight.
         const bool a16 = (reinterpret_cast<uintptr_t>(en.p) & 15u) == 0;
-        const uint32_t S = (wave_any(valid) && wave_all(!valid || a16))
-                               ? __builtin_amdgcn_readfirstlane(
-                                     wave_min(valid ? (en.len >> 7) : 0xffffffffu))
-                               : 0u;
+        const bool all16 = wave_all(!valid || a16);
+        const uint32_t S = bulk_stages(en, valid);
         if constexpr (U == NPROD) {
             // this producer's blocks: k = pidx, pidx + NPROD, ... (one per unit);
             // bulk over the full blocks every lane has, then tail/padding
             const uint32_t K = S * 2u;
             uint32_t B0[16], B1[16];
             uint32_t k = pidx;
-            if constexpr ((V & kVCoop) != 0) {
+            if (!all16) {
+                RawSpan<16> R0, R1;
+                if (pidx < K) load_raw<16>(en.p + 64ull * pidx, R0);
+                if (pidx + NPROD < K) load_raw<16>(en.p + 64ull * (pidx + NPROD), R1);
+                for (; k + NPROD < K; k += 2 * NPROD) {
+                    produce_own_block_any<U, WK, NPROD>(en, k, K, R0, ring, lane);
+                    produce_own_block_any<U, WK, NPROD>(en, k + NPROD, K, R1, ring, lane);
+                }
+                if (k < K) {
+                    produce_own_block_any<U, WK, NPROD>(en, k, K, R0, ring, lane);
+                    k += NPROD;
+                }
+            } else if constexpr ((V & kVCoop) != 0) {
                 const uint4* src[4];
                 coop_sources<4>(A, group, (uint32_t)lane, src);
                 if (pidx < K) coop4_load(src, pidx, B0);
@@ -705,7 +752,19 @@ __device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uin
         }
         // this producer's stages: s = pidx, pidx + NPROD, ...
         uint32_t s = pidx;
-        if constexpr ((V & kVCoop) != 0) {
+        if (!all16) {
+            RawSpan<32> R0, R1;
+            if (pidx < S) load_raw<32>(en.p + 128ull * pidx, R0);
+            if (pidx + NPROD < S) load_raw<32>(en.p + 128ull * (pidx + NPROD), R1);
+            for (; s + NPROD < S; s += 2 * NPROD) {
+                produce_stage_any<U, WK, NPROD>(en, s, S, R0, ring, lane);
+                produce_stage_any<U, WK, NPROD>(en, s + NPROD, S, R1, ring, lane);
+            }
+            if (s < S) {
+                produce_stage_any<U, WK, NPROD>(en, s, S, R0, ring, lane);
+                s += NPROD;
+            }
+        } else if constexpr ((V & kVCoop) != 0) {
             const uint4* src[8];
             coop_sources<8>(A, group, (uint32_t)lane, src);
             uint32_t C0[32], C1[32];
@@ -811,6 +870,36 @@ __device__ __forceinline__ void fused_lane_stages(const Entry& en, uint32_t S, u
     if (s < S) fused_stage<RV>(s, S, en, A0, h);
 }
 
+// The same for a wave whose chunks are not all 16-byte aligned.
+template <int RV>
+__device__ __forceinline__ void fused_stage_any(uint32_t s, uint32_t S, const Entry& en, RawSpan<32>& cur,
+                                                uint32_t (&h)[5]) {
+    const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(en.p) & 3u);
+    uint32_t w[16];
+    shift_raw<32, 0, 16>(cur, sh, w);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
+    compress<RV>(h, w);
+    shift_raw<32, 16, 16>(cur, sh, w);
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
+    if (s + 2 < S) load_raw<32>(en.p + 128ull * (s + 2), cur);
+    compress<RV>(h, w);
+}
+
+template <int RV>
+__device__ __forceinline__ void fused_lane_stages_any(const Entry& en, uint32_t S, uint32_t (&h)[5]) {
+    RawSpan<32> A0, A1;
+    if (S > 0) load_raw<32>(en.p, A0);
+    if (S > 1) load_raw<32>(en.p + 128, A1);
+    uint32_t s = 0;
+    for (; s + 1 < S; s += 2) {
+        fused_stage_any<RV>(s, S, en, A0, h);
+        fused_stage_any<RV>(s + 1, S, en, A1, h);
+    }
+    if (s < S) fused_stage_any<RV>(s, S, en, A0, h);
+}
+
 // RV: round-sum form (sha1_device.hpp round_step); the product uses 0, the
 // A/B library also builds 1 and 2 (SHA1CHUNK_FUSED_VARIANT).
 // The body of one fused wave: message e's lane (group e / 64).
@@ -823,11 +912,11 @@ __device__ __forceinline__ void fused_body(const BatchArgs& A, uint32_t e) {
     uint32_t h[5];
     load_init(A, en.id, h);
     const bool a16 = (reinterpret_cast<uintptr_t>(en.p) & 15u) == 0;
-    const uint32_t S = (wave_any(valid) && wave_all(!valid || a16))
-                           ? __builtin_amdgcn_readfirstlane(
-                                 wave_min(valid ? (en.len >> 7) : 0xffffffffu))
-                           : 0u;
-    fused_lane_stages<RV>(en, S, h);
+    const uint32_t S = bulk_stages(en, valid);
+    if (wave_all(!valid || a16))
+        fused_lane_stages<RV>(en, S, h);
+    else
+        fused_lane_stages_any<RV>(en, S, h);
     if (valid) {
         lane_blocks(A, en, 2u * S, h);
         emit(A, en.id, h);
@@ -871,10 +960,8 @@ __device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, 
     uint32_t h[5];
     load_init(A, en.id, h);
     const bool a16 = (reinterpret_cast<uintptr_t>(en.p) & 15u) == 0;
-    const uint32_t S = (wave_any(valid) && wave_all(!valid || a16))
-                           ? __builtin_amdgcn_readfirstlane(
-                                 wave_min(valid ? (en.len >> 7) : 0xffffffffu))
-                           : 0u;
+    const bool all16 = wave_all(!valid || a16);
+    const uint32_t S = bulk_stages(en, valid);
     // A group whose chunks lie together (in place, or permuted within a
     // span of about their own bytes) streams lane-per-chunk: no UTCL1
     // thrash to avoid there, and the shared loads' LDS round trip costs
@@ -889,7 +976,9 @@ __device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, 
         bytes += (uint64_t)__shfl_xor(bytes, m);
     }
     const bool together = hi - lo <= 2 * bytes + (2ull << 20);
-    if (S > 0 && together) {
+    if (S > 0 && !all16) {  // shared loads need 16-byte aligned chunks
+        fused_lane_stages_any<RV>(en, S, h);
+    } else if (S > 0 && together) {
         fused_lane_stages<RV>(en, S, h);
     } else if (S > 0) {
         const uint4* src[8];

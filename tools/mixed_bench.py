@@ -59,6 +59,9 @@ def main():
                          "adjacent chunks (2 MiB for 512 KiB chunks), or permuted only within each "
                          "window of 64 chunks")
     ap.add_argument("--uniform", type=int, default=0, help="every chunk this long instead of the law")
+    ap.add_argument("--misalign", action="store_true",
+                    help="hash each chunk from 1..15 bytes past its (16-byte aligned) start, 16 bytes "
+                         "shorter: no wave has all lanes 16-byte aligned (the per-lane load path)")
     ap.add_argument("--out", default=None)
     a = ap.parse_args()
     import torch
@@ -84,6 +87,12 @@ def main():
         d_off = torch.from_numpy(off.astype(np.int64)).cuda()
         d_len = torch.from_numpy(lens.astype(np.int32)).cuda()
         pkg.synth_fill_ragged_device(base, d_off, d_len, 0)
+        if a.misalign:
+            shift = (np.arange(n, dtype=np.uint64) % np.uint64(15)) + np.uint64(1)
+            off = off + shift
+            lens = np.maximum(lens.astype(np.int64) - 16, 0).astype(np.uint32)
+            d_off = torch.from_numpy(off.astype(np.int64)).cuda()
+            d_len = torch.from_numpy(lens.astype(np.int32)).cuda()
         nbytes = int(lens.astype(np.uint64).sum())
         ref = None
         for mode in a.modes.split(","):
@@ -136,7 +145,8 @@ def main():
             else:
                 ok = bool(np.array_equal(got, ref))
             sec = float(np.median(ts))
-            row = {"chunks": n, "mode": mode, "layout": a.layout, "uniform": a.uniform, "payload_bytes": nbytes, "ms": round(sec * 1e3, 3),
+            row = {"chunks": n, "mode": mode, "layout": a.layout + ("+misalign" if a.misalign else ""),
+                   "uniform": a.uniform, "payload_bytes": nbytes, "ms": round(sec * 1e3, 3),
                    "payload_GiBps": round(nbytes / sec / 2**30, 2), "runs_ms": [round(t * 1e3, 3) for t in ts],
                    "longest_blocks": int(lens.max()) // 64 + 2, "parity": ok}
             print(json.dumps(row), flush=True)
