@@ -174,31 +174,24 @@ __device__ __forceinline__ void init_state(uint32_t (&h)[5]) {
 // message byte, so they never cross into an unmapped page.  Output: the
 // block's words as LITTLE-endian loads (byte-swap is done by the caller).
 // ---------------------------------------------------------------------------
-// 16-byte-aligned block: 4 x global_load_dwordx4, no branches (so hipcc can
-// count the loads with a partial vmcnt when they are prefetched).
-__device__ __forceinline__ void load_block_a16(const uint8_t* p, uint32_t (&w)[16]) {
-    const uint4* q = reinterpret_cast<const uint4*>(p);
+// A full block: 4 x global_load_dwordx4 of exactly its 64 bytes, no
+// branches (so hipcc can count the loads with a partial vmcnt when they are
+// prefetched), at any byte alignment: gfx950 under ROCm runs in unaligned
+// access mode (hipcc emits global_load_dwordx4 for this align-1 type, and
+// byte-unaligned loads read correctly on MI355X), so a chunk's bulk loads
+// need not care where it starts.
+typedef uint32_t u32x4u __attribute__((ext_vector_type(4), aligned(1)));
+
+__device__ __forceinline__ void load_block16(const uint8_t* p, uint32_t (&w)[16]) {
+    const u32x4u* q = reinterpret_cast<const u32x4u*>(p);
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-        const uint4 x = q[j];
+        const u32x4u x = q[j];
         w[4 * j + 0] = x.x;
         w[4 * j + 1] = x.y;
         w[4 * j + 2] = x.z;
         w[4 * j + 3] = x.w;
     }
-}
-
-// Any alignment: 16 (+1) aligned dword loads and v_alignbyte funnel shifts.
-__device__ __forceinline__ void load_block_any(const uint8_t* p, uint32_t (&w)[16]) {
-    const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-    const uint32_t sh = static_cast<uint32_t>(a & 3u);
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
-    uint32_t d[17];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) d[j] = q[j];
-    d[16] = sh ? q[16] : 0u;
-#pragma unroll
-    for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], sh);
 }
 
 // K dwords from any byte alignment, loaded raw now and shifted at use (so a

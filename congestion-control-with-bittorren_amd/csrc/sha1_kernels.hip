@@ -85,23 +85,14 @@ __device__ __forceinline__ void emit(const BatchArgs& A, uint32_t id, const uint
     }
 }
 
-// Blocks [k0, nfull) of one lane straight from global memory, then the
-// padded tail (unless the batch is in update mode).  A16 selects the
-// branch-free 16-byte-aligned loader (chosen per wave), so the one-block
-// register prefetch is counted with a partial vmcnt.
-template <bool A16>
+// Blocks [k0, nfull) of one lane straight from global memory (one block
+// prefetched), then the padded tail (unless the batch is in update mode).
 __device__ __forceinline__ void lane_loop(const Entry& en, uint32_t k0, uint32_t (&h)[5]) {
     const uint32_t nfull = en.len >> 6;
     uint32_t cur[16], nxt[16];
-    if (k0 < nfull) {
-        if constexpr (A16) load_block_a16(en.p + 64ull * k0, cur);
-        else load_block_any(en.p + 64ull * k0, cur);
-    }
+    if (k0 < nfull) load_block16(en.p + 64ull * k0, cur);
     for (uint32_t k = k0; k < nfull; ++k) {
-        if (k + 1 < nfull) {
-            if constexpr (A16) load_block_a16(en.p + 64ull * (k + 1), nxt);
-            else load_block_any(en.p + 64ull * (k + 1), nxt);
-        }
+        if (k + 1 < nfull) load_block16(en.p + 64ull * (k + 1), nxt);
         uint32_t w[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) w[j] = bswap(cur[j]);
@@ -116,11 +107,7 @@ __device__ __forceinline__ bool wave_any(bool x) { return __ballot(x) != 0; }
 
 __device__ __forceinline__ void lane_blocks(const BatchArgs& A, const Entry& en, uint32_t k0,
                                             uint32_t (&h)[5]) {
-    const bool a16 = (reinterpret_cast<uintptr_t>(en.p) & 15u) == 0;
-    if (wave_all(a16))
-        lane_loop<true>(en, k0, h);
-    else
-        lane_loop<false>(en, k0, h);
+    lane_loop(en, k0, h);
     const uint32_t nfull = en.len >> 6;
     if (!A.out_state)
         finish_message(h, en.p + 64ull * nfull, en.len & 63u, A.prefix_bytes + en.len);
@@ -220,7 +207,7 @@ __device__ __forceinline__ void tail_block_words(const Entry& en, uint32_t k, ui
     const uint32_t nfull = en.len >> 6, rem = en.len & 63u;
     const uint64_t bits = (uint64_t)en.len * 8ull;
     if (k < nfull) {
-        load_block_any(en.p + 64ull * k, w);
+        load_block16(en.p + 64ull * k, w);
 #pragma unroll
         for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
     } else if (k == nfull) {
@@ -262,14 +249,19 @@ __device__ __forceinline__ void produce_block(uint32_t k, uint32_t (&w)[16], uin
 struct Stage {
     uint32_t w[32];
 };
+// V: uint4 when every lane's chunk is 16-byte aligned (hipcc then keeps
+// the stage in 64-bit register pairs: 8 fewer moves per block in the fused
+// loop), u32x4u at any alignment.
+template <typename V = u32x4u>
 __device__ __forceinline__ void load_stage(const uint8_t* p, Stage& st) {
-    uint32_t a[16], b[16];
-    load_block_a16(p, a);
-    load_block_a16(p + 64, b);
+    const V* q = reinterpret_cast<const V*>(p);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-        st.w[j] = a[j];
-        st.w[16 + j] = b[j];
+    for (int j = 0; j < 8; ++j) {
+        const V x = q[j];
+        st.w[4 * j + 0] = x.x;
+        st.w[4 * j + 1] = x.y;
+        st.w[4 * j + 2] = x.z;
+        st.w[4 * j + 3] = x.w;
     }
 }
 
@@ -300,10 +292,10 @@ __device__ __forceinline__ uint32_t coop_slot(uint32_t c, uint32_t piece) {
 
 // (the in-flight stage lives in plain 32-bit words: an array of uint4
 // stays in scratch memory)
-__device__ __forceinline__ void coop_load(const uint4* const (&src)[8], uint32_t s, uint32_t (&v)[32]) {
+__device__ __forceinline__ void coop_load(const u32x4u* const (&src)[8], uint32_t s, uint32_t (&v)[32]) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-        const uint4 x = src[i][8u * s];
+        const u32x4u x = src[i][8u * s];
         v[4 * i + 0] = x.x;
         v[4 * i + 1] = x.y;
         v[4 * i + 2] = x.z;
@@ -336,10 +328,10 @@ __device__ __forceinline__ void coop_read(const uint8_t* buf, uint32_t lane, uin
 // l%4), staged through 4 KiB of LDS.  Piece p of chunk c at
 // c*64 + ((p + c/4) & 3)*16: conflict-free b128 stores and reads, and a
 // lane's store address is the same for every i but for an i*1024 offset.
-__device__ __forceinline__ void coop4_load(const uint4* const (&src)[4], uint32_t k, uint32_t (&v)[16]) {
+__device__ __forceinline__ void coop4_load(const u32x4u* const (&src)[4], uint32_t k, uint32_t (&v)[16]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-        const uint4 x = src[i][4u * k];
+        const u32x4u x = src[i][4u * k];
         v[4 * i + 0] = x.x;
         v[4 * i + 1] = x.y;
         v[4 * i + 2] = x.z;
@@ -372,11 +364,11 @@ __device__ __forceinline__ void coop4_read(const uint8_t* buf, uint32_t lane, ui
 // and at least as long as the wave's bulk region).
 template <int LANES>
 __device__ __forceinline__ void coop_sources(const BatchArgs& A, uint32_t group, uint32_t lane,
-                                             const uint4* (&src)[LANES]) {
+                                             const u32x4u* (&src)[LANES]) {
 #pragma unroll
     for (uint32_t i = 0; i < (uint32_t)LANES; ++i) {
         const uint32_t ej = group * 64u + (64u / LANES) * i + lane / LANES;
-        src[i] = reinterpret_cast<const uint4*>(fetch_entry(A, ej < A.n ? ej : group * 64u).p) + (lane % LANES);
+        src[i] = reinterpret_cast<const u32x4u*>(fetch_entry(A, ej < A.n ? ej : group * 64u).p) + (lane % LANES);
     }
 }
 
@@ -402,7 +394,7 @@ __device__ __forceinline__ void produce_stage(const Entry& en, uint32_t s, uint3
 // follow; the wave's LDS accesses complete in order, so the transposing
 // reads precede the W writes over them).
 template <int U, bool WK, int NPROD = 1>
-__device__ __forceinline__ void produce_stage_coop(const uint4* const (&src)[8], uint32_t s, uint32_t S,
+__device__ __forceinline__ void produce_stage_coop(const u32x4u* const (&src)[8], uint32_t s, uint32_t S,
                                                    uint32_t (&cur)[32], uint8_t* ring, uint32_t lane) {
     const uint32_t k0 = 2 * s, m = k0 / U, j = k0 - m * U;
     uint8_t* raw = ring + ((m & 1u) * U + j) * kWBlockBytes;
@@ -420,7 +412,7 @@ __device__ __forceinline__ void produce_stage_coop(const uint4* const (&src)[8],
 }
 
 template <int U, bool WK, int NPROD>
-__device__ __forceinline__ void produce_own_block_coop(const uint4* const (&src)[4], uint32_t k, uint32_t K,
+__device__ __forceinline__ void produce_own_block_coop(const u32x4u* const (&src)[4], uint32_t k, uint32_t K,
                                                        uint32_t (&cur)[16], uint8_t* ring, uint32_t lane) {
     const uint32_t m = k / U, j = k - m * U;
     uint8_t* raw = ring + ((m & 1u) * U + j) * kWBlockBytes;
@@ -433,37 +425,6 @@ __device__ __forceinline__ void produce_own_block_coop(const uint4* const (&src)
     produce_block<U, WK, NPROD>(k, w, ring, (int)lane);
 }
 
-// The same two producers for a wave whose chunks are not all 16-byte
-// aligned: loads of any alignment (RawSpan: dwords from p & ~3, shifted by
-// p & 3 at use), with the same registers-ahead prefetch.
-template <int U, bool WK, int NPROD = 1>
-__device__ __forceinline__ void produce_stage_any(const Entry& en, uint32_t s, uint32_t S, RawSpan<32>& cur,
-                                                  uint8_t* ring, int lane) {
-    const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(en.p) & 3u);
-    uint32_t w[16];
-    shift_raw<32, 0, 16>(cur, sh, w);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
-    produce_block<U, WK, NPROD>(2 * s, w, ring, lane);
-    shift_raw<32, 16, 16>(cur, sh, w);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
-    if (s + 2 * NPROD < S) load_raw<32>(en.p + 128ull * (s + 2 * NPROD), cur);
-    produce_block<U, WK, NPROD>(2 * s + 1, w, ring, lane);
-}
-
-template <int U, bool WK, int NPROD>
-__device__ __forceinline__ void produce_own_block_any(const Entry& en, uint32_t k, uint32_t K, RawSpan<16>& cur,
-                                                      uint8_t* ring, int lane) {
-    const uint32_t sh = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(en.p) & 3u);
-    uint32_t w[16];
-    shift_raw<16>(cur, sh, w);
-#pragma unroll
-    for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
-    if (k + 2 * NPROD < K) load_raw<16>(en.p + 64ull * (k + 2 * NPROD), cur);
-    produce_block<U, WK, NPROD>(k, w, ring, lane);
-}
-
 // Producer that owns one block per unit (U == NPROD): block k from `cur`,
 // which is then refilled with this producer's block after next, k + 2 NPROD.
 template <int U, bool WK, int NPROD>
@@ -472,7 +433,7 @@ __device__ __forceinline__ void produce_own_block(const Entry& en, uint32_t k, u
     uint32_t w[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) w[j] = bswap(cur[j]);
-    if (k + 2 * NPROD < K) load_block_a16(en.p + 64ull * (k + 2 * NPROD), cur);
+    if (k + 2 * NPROD < K) load_block16(en.p + 64ull * (k + 2 * NPROD), cur);
     produce_block<U, WK, NPROD>(k, w, ring, lane);
 }
 
@@ -693,11 +654,8 @@ __device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uin
     if (producer) {
         // ----------------------------- producer -------------------------
         // Bulk: stages (2 full blocks) that every lane has, with
-        // branch-free loads hipcc can count (16-byte ones when every lane's
-        // chunk is 16-byte aligned, dword + funnel-shift ones otherwise);
-        // registers hold the current stage and the next one in flight.
-        const bool a16 = (reinterpret_cast<uintptr_t>(en.p) & 15u) == 0;
-        const bool all16 = wave_all(!valid || a16);
+        // branch-free loads hipcc can count (of any alignment); registers
+        // hold the current stage and the next one in flight.
         const uint32_t S = bulk_stages(en, valid);
         if constexpr (U == NPROD) {
             // this producer's blocks: k = pidx, pidx + NPROD, ... (one per unit);
@@ -705,20 +663,8 @@ __device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uin
             const uint32_t K = S * 2u;
             uint32_t B0[16], B1[16];
             uint32_t k = pidx;
-            if (!all16) {
-                RawSpan<16> R0, R1;
-                if (pidx < K) load_raw<16>(en.p + 64ull * pidx, R0);
-                if (pidx + NPROD < K) load_raw<16>(en.p + 64ull * (pidx + NPROD), R1);
-                for (; k + NPROD < K; k += 2 * NPROD) {
-                    produce_own_block_any<U, WK, NPROD>(en, k, K, R0, ring, lane);
-                    produce_own_block_any<U, WK, NPROD>(en, k + NPROD, K, R1, ring, lane);
-                }
-                if (k < K) {
-                    produce_own_block_any<U, WK, NPROD>(en, k, K, R0, ring, lane);
-                    k += NPROD;
-                }
-            } else if constexpr ((V & kVCoop) != 0) {
-                const uint4* src[4];
+            if constexpr ((V & kVCoop) != 0) {
+                const u32x4u* src[4];
                 coop_sources<4>(A, group, (uint32_t)lane, src);
                 if (pidx < K) coop4_load(src, pidx, B0);
                 if (pidx + NPROD < K) coop4_load(src, pidx + NPROD, B1);
@@ -731,8 +677,8 @@ __device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uin
                     k += NPROD;
                 }
             } else {
-                if (pidx < K) load_block_a16(en.p + 64ull * pidx, B0);
-                if (pidx + NPROD < K) load_block_a16(en.p + 64ull * (pidx + NPROD), B1);
+                if (pidx < K) load_block16(en.p + 64ull * pidx, B0);
+                if (pidx + NPROD < K) load_block16(en.p + 64ull * (pidx + NPROD), B1);
                 for (; k + NPROD < K; k += 2 * NPROD) {
                     produce_own_block<U, WK, NPROD>(en, k, K, B0, ring, lane);
                     produce_own_block<U, WK, NPROD>(en, k + NPROD, K, B1, ring, lane);
@@ -752,20 +698,8 @@ __device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uin
         }
         // this producer's stages: s = pidx, pidx + NPROD, ...
         uint32_t s = pidx;
-        if (!all16) {
-            RawSpan<32> R0, R1;
-            if (pidx < S) load_raw<32>(en.p + 128ull * pidx, R0);
-            if (pidx + NPROD < S) load_raw<32>(en.p + 128ull * (pidx + NPROD), R1);
-            for (; s + NPROD < S; s += 2 * NPROD) {
-                produce_stage_any<U, WK, NPROD>(en, s, S, R0, ring, lane);
-                produce_stage_any<U, WK, NPROD>(en, s + NPROD, S, R1, ring, lane);
-            }
-            if (s < S) {
-                produce_stage_any<U, WK, NPROD>(en, s, S, R0, ring, lane);
-                s += NPROD;
-            }
-        } else if constexpr ((V & kVCoop) != 0) {
-            const uint4* src[8];
+        if constexpr ((V & kVCoop) != 0) {
+            const u32x4u* src[8];
             coop_sources<8>(A, group, (uint32_t)lane, src);
             uint32_t C0[32], C1[32];
             if (pidx < S) coop_load(src, pidx, C0);
@@ -843,7 +777,7 @@ __global__ __launch_bounds__((kSplitThreads<PAIRS, V, NPROD>)) void sha1_split_k
 // kernel's LDS hand-off is pure overhead.  Each lane streams its own chunk
 // with 16-byte loads, two 128-byte stages (4 blocks) in flight in VGPRs so
 // HBM latency under full load stays covered.
-template <int RV>
+template <int RV, typename V>
 __device__ __forceinline__ void fused_stage(uint32_t s, uint32_t S, const Entry& en, Stage& cur,
                                             uint32_t (&h)[5]) {
 #pragma unroll
@@ -851,26 +785,29 @@ __device__ __forceinline__ void fused_stage(uint32_t s, uint32_t S, const Entry&
         uint32_t w[16];
 #pragma unroll
         for (int j = 0; j < 16; ++j) w[j] = bswap(cur.w[16 * half + j]);
-        if (half == 1 && s + 2 < S) load_stage(en.p + 128ull * (s + 2), cur);
+        if (half == 1 && s + 2 < S) load_stage<V>(en.p + 128ull * (s + 2), cur);
         compress<RV>(h, w);
     }
 }
 
 // Stages 0 .. S-1 of every lane's chunk, each lane loading its own.
-template <int RV>
-__device__ __forceinline__ void fused_lane_stages(const Entry& en, uint32_t S, uint32_t (&h)[5]) {
+template <int RV, typename V>
+__device__ __forceinline__ void fused_lane_stages_v(const Entry& en, uint32_t S, uint32_t (&h)[5]) {
     Stage A0, A1;
-    if (S > 0) load_stage(en.p, A0);
-    if (S > 1) load_stage(en.p + 128, A1);
+    if (S > 0) load_stage<V>(en.p, A0);
+    if (S > 1) load_stage<V>(en.p + 128, A1);
     uint32_t s = 0;
     for (; s + 1 < S; s += 2) {
-        fused_stage<RV>(s, S, en, A0, h);
-        fused_stage<RV>(s + 1, S, en, A1, h);
+        fused_stage<RV, V>(s, S, en, A0, h);
+        fused_stage<RV, V>(s + 1, S, en, A1, h);
     }
-    if (s < S) fused_stage<RV>(s, S, en, A0, h);
+    if (s < S) fused_stage<RV, V>(s, S, en, A0, h);
 }
 
-// The same for a wave whose chunks are not all 16-byte aligned.
+// The same for a wave whose chunks are not all 16-byte aligned: dword loads
+// (RawSpan, from p & ~3) two stages ahead, funnel-shifted by p & 3 at use.
+// Lane-per-chunk byte-unaligned 16-byte loads were slower here (65536 x
+// 512 KiB 1..15 bytes off: 13.6 ms against 11.2; profiles/misaligned_r02.json).
 template <int RV>
 __device__ __forceinline__ void fused_stage_any(uint32_t s, uint32_t S, const Entry& en, RawSpan<32>& cur,
                                                 uint32_t (&h)[5]) {
@@ -900,6 +837,14 @@ __device__ __forceinline__ void fused_lane_stages_any(const Entry& en, uint32_t 
     if (s < S) fused_stage_any<RV>(s, S, en, A0, h);
 }
 
+template <int RV>
+__device__ __forceinline__ void fused_lane_stages(const Entry& en, bool valid, uint32_t S, uint32_t (&h)[5]) {
+    if (wave_all(!valid || (reinterpret_cast<uintptr_t>(en.p) & 15u) == 0))
+        fused_lane_stages_v<RV, uint4>(en, S, h);
+    else
+        fused_lane_stages_any<RV>(en, S, h);
+}
+
 // RV: round-sum form (sha1_device.hpp round_step); the product uses 0, the
 // A/B library also builds 1 and 2 (SHA1CHUNK_FUSED_VARIANT).
 // The body of one fused wave: message e's lane (group e / 64).
@@ -911,12 +856,8 @@ __device__ __forceinline__ void fused_body(const BatchArgs& A, uint32_t e) {
     if (!valid) en.len = 0;
     uint32_t h[5];
     load_init(A, en.id, h);
-    const bool a16 = (reinterpret_cast<uintptr_t>(en.p) & 15u) == 0;
     const uint32_t S = bulk_stages(en, valid);
-    if (wave_all(!valid || a16))
-        fused_lane_stages<RV>(en, S, h);
-    else
-        fused_lane_stages_any<RV>(en, S, h);
+    fused_lane_stages<RV>(en, valid, S, h);
     if (valid) {
         lane_blocks(A, en, 2u * S, h);
         emit(A, en.id, h);
@@ -959,8 +900,6 @@ __device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, 
     if (!valid) en.len = 0;
     uint32_t h[5];
     load_init(A, en.id, h);
-    const bool a16 = (reinterpret_cast<uintptr_t>(en.p) & 15u) == 0;
-    const bool all16 = wave_all(!valid || a16);
     const uint32_t S = bulk_stages(en, valid);
     // A group whose chunks lie together (in place, or permuted within a
     // span of about their own bytes) streams lane-per-chunk: no UTCL1
@@ -976,12 +915,10 @@ __device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, 
         bytes += (uint64_t)__shfl_xor(bytes, m);
     }
     const bool together = hi - lo <= 2 * bytes + (2ull << 20);
-    if (S > 0 && !all16) {  // shared loads need 16-byte aligned chunks
-        fused_lane_stages_any<RV>(en, S, h);
-    } else if (S > 0 && together) {
-        fused_lane_stages<RV>(en, S, h);
-    } else if (S > 0) {
-        const uint4* src[8];
+    if (S > 0 && together && wave_all(!valid || (reinterpret_cast<uintptr_t>(en.p) & 15u) == 0)) {
+        fused_lane_stages_v<RV, uint4>(en, S, h);
+    } else if (S > 0) {  // scattered or not 16-byte aligned: shared loads (any alignment)
+        const u32x4u* src[8];
         coop_sources<8>(A, group, lane, src);
         // stage loads run ahead unconditionally (clamped to the last stage:
         // a repeated read at the end, never past a chunk)
