@@ -270,7 +270,8 @@ __device__ __forceinline__ void load_stage(const uint8_t* p, Stage& st) {
 // (i = 0..7) of a 128-byte stage reads 128 bytes of each of the group's
 // chunks 8i .. 8i+7 (lane l: chunk 8i + l/8, 16-byte piece l%8), so one load
 // instruction touches 8 chunks instead of 64, and an LDS transpose hands
-// each lane its own chunk's 128 bytes.  The lane-per-chunk pattern makes
+// each lane its own chunk's 128 bytes.  The loads take chunks at any byte
+// alignment (u32x4u, sha1_device.hpp).  The lane-per-chunk pattern makes
 // each load instruction translate 64 addresses; with chunks far apart that
 // thrashes the CU's translation cache: scattered 512 KiB chunks read at
 // 1183 GB/s lane-per-chunk and 5954 GB/s 8 chunks per instruction (5036 /
@@ -775,7 +776,8 @@ __global__ __launch_bounds__((kSplitThreads<PAIRS, V, NPROD>)) void sha1_split_k
 // block).  Best once there are enough chunks for two or more waves per SIMD:
 // then the SIMD, not one wave's issue rate, is the limit and the split
 // kernel's LDS hand-off is pure overhead.  Each lane streams its own chunk
-// with 16-byte loads, two 128-byte stages (4 blocks) in flight in VGPRs so
+// with 16-byte loads (dword loads shifted at use when the wave's chunks are
+// not all 16-byte aligned), two 128-byte stages (4 blocks) in flight in VGPRs so
 // HBM latency under full load stays covered.
 template <int RV, typename V>
 __device__ __forceinline__ void fused_stage(uint32_t s, uint32_t S, const Entry& en, Stage& cur,
