@@ -4,7 +4,8 @@ producers, 8 or 4 lanes per chunk; the mixed kernel's fused tail, 8 lanes per
 chunk): each load instruction then reads pieces of 8 or 16 chunks that lie
 far apart, and the LDS transpose must hand every lane its own chunk's bytes.
 Partial last groups exercise the slots past the batch (they read the
-group's first chunk).  Bit-exact against the oracle."""
+group's first chunk); byte-packed chunks (align 1) the shared loads' any
+alignment.  Bit-exact against the oracle."""
 import numpy as np
 import pytest
 
@@ -54,8 +55,9 @@ def _check(got, want, what):
     assert bad.size == 0, f"{what}: {bad.size} bad digests, first {bad[:8]}"
 
 
+@pytest.mark.parametrize("align", [16, 1])
 @pytest.mark.parametrize("unit", ["4", "11", "1"])
-def test_split_shapes_scattered(pkg, dev, oracle, monkeypatch, unit):
+def test_split_shapes_scattered(pkg, dev, oracle, monkeypatch, unit, align):
     """Equal-ish 9 KiB chunks (a few ragged tails) in a random order, three
     and a half groups: the one-group (unit 4), 8-wave (unit 11) and 1-block
     (unit 1, lane-per-chunk loads) split shapes."""
@@ -64,13 +66,14 @@ def test_split_shapes_scattered(pkg, dev, oracle, monkeypatch, unit):
     n = 64 * 3 + 37
     lens = np.full(n, 9216, np.uint32)
     lens[rng.choice(n, 20, replace=False)] = rng.integers(8000, 9300, 20)
-    host, off = _scattered(rng, n, lens)
+    host, off = _scattered(rng, n, lens, align)
     want = oracle.hash_batch(host, off, lens)
     got = _run(pkg, torch, host, off, lens, "split", {"SHA1CHUNK_SPLIT_UNIT": unit}, monkeypatch)
-    _check(got, want, f"split unit {unit}")
+    _check(got, want, f"split unit {unit} align {align}")
 
 
-def test_mixed_plans_scattered(pkg, dev, oracle, cus, monkeypatch):
+@pytest.mark.parametrize("align", [16, 1])
+def test_mixed_plans_scattered(pkg, dev, oracle, cus, monkeypatch, align):
     """A ragged batch of more groups than CUs in a random memory order (so
     every sorted group's chunks lie far apart) through the device plan, the
     all-fused tail at F = 4 and 8, a split head, all-split and the 8-wave
@@ -81,8 +84,8 @@ def test_mixed_plans_scattered(pkg, dev, oracle, cus, monkeypatch):
     n = 64 * G - 29
     lens = rng.integers(0, 5000, n).astype(np.uint32)
     lens[rng.choice(n, 3 * cus, replace=False)] = rng.integers(9000, 30000, 3 * cus)
-    host, off = _scattered(rng, n, lens)
+    host, off = _scattered(rng, n, lens, align)
     want = oracle.hash_batch(host, off, lens)
     for p in (None, "0,0,4", "0,0,8", "0,17,4", f"0,{G},4", "1,0,0"):
         got = _run(pkg, torch, host, off, lens, "auto", {"SHA1CHUNK_MIXED_PLAN": p} if p else {}, monkeypatch)
-        _check(got, want, f"plan {p or 'device'}")
+        _check(got, want, f"plan {p or 'device'} align {align}")
