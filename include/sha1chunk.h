@@ -52,7 +52,7 @@ enum {
     SHA1CHUNK_KERNEL_AUTO = 0,
     SHA1CHUNK_KERNEL_LANE = 1,  /* one lane per chunk, per-lane loads; any alignment   */
     SHA1CHUNK_KERNEL_FUSED = 2, /* one lane per chunk, schedule + rounds in registers,
-                                   two 128-byte stages of per-lane 16-byte loads ahead */
+                                   two 128-byte stages of per-lane loads ahead       */
     SHA1CHUNK_KERNEL_SPLIT = 3  /* schedule-producer + round-consumer wave pairs        */
 };
 
@@ -67,7 +67,9 @@ int sha1chunk_verify_batch(const void *base, const uint64_t *offsets, const uint
                            size_t n, const uint8_t *expected, uint8_t *mismatch, unsigned flags);
 
 /* Device-resident, asynchronous on `stream` (a hipStream_t, NULL = default).
- * All pointers are device pointers.  Returns after enqueueing. */
+ * All pointers are device pointers.  Returns after enqueueing.  Chunks may
+ * start at any byte and lie anywhere in the buffer (16-byte aligned starts
+ * are ~10 % faster in the fused shapes; placement costs nothing). */
 int sha1chunk_hash_device_async(const void *d_base, const uint64_t *d_offsets,
                                 const uint32_t *d_lengths, size_t n, uint8_t *d_digests,
                                 void *stream, int kernel);
