@@ -41,22 +41,23 @@ public:
     size_t width() const { return th_.size() + 1; }
     // fn(i) for i in [0, parts), on the caller and the helpers
     void run(size_t parts, const std::function<void(size_t)>& fn) {
-        if (parts <= 1 || th_.empty()) {
+        if (parts <= 1 || th_.empty() || parts > 0xffffffffu) {
             for (size_t i = 0; i < parts; ++i) fn(i);
             return;
         }
         {
             std::lock_guard<std::mutex> g(mu_);
             fn_ = &fn;
-            parts_.store(parts);
+            parts_ = parts;
             left_.store(parts);
-            next_.store(0);
-            gen_.fetch_add(1);
+            job_ = gen_.load() + 1;
+            next_.store((job_ & 0xffffffffu) << 32);
+            gen_.store(job_);
         }
         // helpers still polling see gen_ at once; only sleeping ones need the
         // (syscall) wake-up
         if (sleepers_.load() > 0) cv_.notify_all();
-        work();
+        work(job_, parts, &fn);
         // the caller's own parts are done; wait for the helpers' parts
         for (int spin = 0; left_.load() != 0 && spin < 200000; ++spin) cpu_relax();
         if (left_.load() != 0) {
@@ -67,13 +68,21 @@ public:
 
 private:
     static constexpr int kSpin = 20000;  // pause loops (tens of microseconds)
-    void work() {
-        for (size_t i; (i = next_.fetch_add(1)) < parts_.load();) {
-            (*fn_)(i);
+    // Claims part indices of job `job` only: the counter carries the job
+    // number in its high half, so a helper that finished (or never started)
+    // an older job cannot claim an index of the next one, and every part of a
+    // job runs exactly once.
+    void work(uint64_t job, size_t parts, const std::function<void(size_t)>* fn) {
+        uint64_t cur = next_.load();
+        for (;;) {
+            if ((cur >> 32) != (job & 0xffffffffu) || (cur & 0xffffffffu) >= parts) return;
+            if (!next_.compare_exchange_weak(cur, cur + 1)) continue;
+            (*fn)(size_t(cur & 0xffffffffu));
             if (left_.fetch_sub(1) == 1) {
                 std::lock_guard<std::mutex> g(mu_);
                 done_.notify_all();
             }
+            cur = next_.load();
         }
     }
     void loop() {
@@ -88,12 +97,17 @@ private:
                 sleepers_.fetch_sub(1);
             }
             if (stop_.load()) return;
+            uint64_t job;
+            size_t parts;
+            const std::function<void(size_t)>* fn;
             {
                 // a job's fields are published under mu_
                 std::lock_guard<std::mutex> g(mu_);
-                seen = gen_.load();
+                seen = job = gen_.load();
+                parts = parts_;
+                fn = fn_;
             }
-            work();
+            work(job, parts, fn);
         }
     }
     std::vector<std::thread> th_;
@@ -103,8 +117,9 @@ private:
     std::atomic<int> sleepers_{0};
     std::atomic<bool> stop_{false};
     const std::function<void(size_t)>* fn_ = nullptr;
-    std::atomic<size_t> parts_{0};
-    std::atomic<size_t> next_{0};
+    size_t parts_ = 0;      // guarded by mu_
+    uint64_t job_ = 0;      // caller side only
+    std::atomic<uint64_t> next_{0};  // job << 32 | next part index
     std::atomic<size_t> left_{0};
 };
 
