@@ -116,3 +116,62 @@ def test_random_batches_mixed_kernel(pkg, dev, oracle, seed, monkeypatch):
         assert bad.size == 0, f"seed {seed} plan {p or 'device'} n={n} align={align}: {bad.size} bad, " \
                               f"first {bad[:6]} lens {lens[bad[:6]]}"
     monkeypatch.delenv("SHA1CHUNK_MIXED_PLAN", raising=False)
+
+
+# The receive path's verify queue (sha1chunk_vq_*, the batched verify_hash of
+# job.c:217-228): random interleavings of submit / non-blocking poll / flush /
+# partial drains with a small result buffer, random batch sizes, growth on or
+# off and 1 or 4 copy threads (chunks above 64 KiB are copied in pieces by the
+# copy pool).  Every tag must come back exactly once with verify_hash's 0/1,
+# and pending must count what is still owed.
+@pytest.mark.parametrize("seed", range(int(os.environ.get("SHA1CHUNK_FUZZ_SEEDS", "12")) // 2 + 1))
+def test_random_verify_queue_interleavings(pkg, dev, oracle, seed, monkeypatch):
+    import time
+    rng = np.random.default_rng(9900 + seed)
+    monkeypatch.setenv("SHA1CHUNK_VQ_GROW", str(int(rng.integers(0, 2))))
+    monkeypatch.setenv("SHA1CHUNK_VQ_THREADS", str(int(rng.choice([1, 4]))))
+    batch = int(rng.choice([1, 3, 8, 32, 100]))
+    maxlen = int(rng.choice([200000, 524288]))
+    n = int(rng.integers(1, 260))
+    lens = np.minimum(_lengths(rng, n), maxlen)
+    data = rng.integers(0, 256, int(lens.max()) + 4096, dtype=np.uint8)
+    want, got, owed = {}, {}, 0
+    with pkg.VerifyQueue(batch=batch, max_chunk_len=maxlen) as q:
+        for t in range(n):
+            start = int(rng.integers(0, 4096))
+            chunk = data[start:start + int(lens[t])].tobytes()
+            dig = oracle.shahash(chunk)
+            bad = bool(rng.random() < 0.25)
+            if bad:
+                k = int(rng.integers(0, 20))
+                dig = dig[:k] + bytes([dig[k] ^ (1 << int(rng.integers(0, 8)))]) + dig[k + 1:]
+            tag = int(rng.integers(0, 1 << 62)) * 4 + t % 4  # sparse, unordered tags
+            while tag in want:
+                tag += 4
+            want[tag] = int(bad)
+            q.submit(chunk, dig, tag)
+            owed += 1
+            op = rng.random()
+            if op < 0.3:
+                res = q.poll(max_results=int(rng.integers(1, 8)))
+            elif op < 0.4:
+                q.flush()
+                res = []
+            elif op < 0.45:
+                res = q.poll(wait=True, max_results=int(rng.integers(1, 64)))
+            else:
+                res = []
+            for tg, m in res:
+                assert tg not in got, f"seed {seed}: tag returned twice"
+                got[tg] = m
+            owed -= len(res)
+            assert q.pending == owed
+        t0 = time.time()
+        while q.pending and time.time() - t0 < 60:
+            res = q.poll(wait=bool(rng.integers(0, 2)), max_results=int(rng.integers(1, 50)))
+            for tg, m in res:
+                assert tg not in got, f"seed {seed}: tag returned twice"
+                got[tg] = m
+        assert q.pending == 0
+    assert got == want, f"seed {seed} batch {batch} n {n}: " \
+                        f"{sum(got.get(k) != v for k, v in want.items())} wrong"
