@@ -1335,7 +1335,7 @@ bool split_unit_built(int u) {
 #ifdef SHA1CHUNK_AB_VARIANTS
     static const int built[] = {1,  2,  3,  4,  8,  9,  10, 11, 12, 20, 21, 22, 23, 24, 26, 27,
                                 30, 31, 32, 33, 34, 36, 37, 42, 44, 45, 46, 504, 505, 506, 507,
-                                569, 577, 578, 579, 580, 581, 13, 583, 584, 585};
+                                569, 577, 578, 579, 580, 581, 13, 583, 584, 585, 86, 87};
     for (int b : built)
         if (u == b) return true;
     return false;
@@ -1423,6 +1423,14 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
 
     case 8:  // 4 pairs per workgroup (512 threads), one consumer + producer per SIMD
         hipLaunchKernelGGL((sha1_split_kernel<1, 4>), dim3((groups + 3) / 4), dim3(512), 0, st, A);
+        break;
+    case 86:  // case 8 with shared producer loads (4 groups per CU, A/B vs fused)
+        hipLaunchKernelGGL((sha1_split_kernel<1, 4, kVWK | kVUnmask | kVCoop>), dim3((groups + 3) / 4), dim3(512),
+                           0, st, A);
+        break;
+    case 87:  // case 86 with K added in the consumer (cheaper producer)
+        hipLaunchKernelGGL((sha1_split_kernel<1, 4, kVUnmask | kVCoop>), dim3((groups + 3) / 4), dim3(512), 0,
+                           st, A);
         break;
     case 10:  // 2 pairs x (consumer + 2 producers), 2-block units, 8-wave layout
         hipLaunchKernelGGL((sha1_split_kernel<2, 2, kVWK | kVUnmask | kVLayout8, 2>), dim3((groups + 1) / 2),
