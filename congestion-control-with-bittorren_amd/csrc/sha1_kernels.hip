@@ -196,6 +196,47 @@ struct SchedWrite {
     }
 };
 
+// Global-memory W ring (A/B flag kVGlobalW, defined with the variant flags).
+typedef uint32_t gw_u4 __attribute__((ext_vector_type(4)));
+struct GRing {
+    __amdgpu_buffer_rsrc_t r;
+    uint32_t base;  // byte offset of this group's ring
+};
+__device__ __forceinline__ void gw_barrier() {
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0) lgkmcnt(0) (gfx9 encoding)
+    asm volatile("s_barrier" ::: "memory");
+}
+template <int T, bool WK>
+struct SchedWriteG {
+    __device__ __forceinline__ static void run(uint32_t (&w)[16], const GRing& g, uint32_t off, int lane) {
+        if constexpr (T < 80) {
+            if constexpr (T >= 16) sched_step<T>(w);
+            if constexpr ((T & 3) == 3) {
+                constexpr int j = (T - 3) & 15;
+                constexpr uint32_t k = WK ? round_k<T>() : 0u;
+                gw_u4 x = {w[j] + k, w[j + 1] + k, w[j + 2] + k, w[j + 3] + k};
+                __builtin_amdgcn_raw_buffer_store_b128(x, g.r, (int)(g.base + off + (T >> 2) * 1024 + lane * 16), 0,
+                                                       16);
+            }
+            SchedWriteG<T + 1, WK>::run(w, g, off, lane);
+        }
+    }
+};
+template <int P>
+__device__ __forceinline__ void read_w_group_g(const GRing& g, uint32_t off, uint32_t lane, uint32_t (&W)[80]) {
+#pragma unroll
+    for (int q = 5 * P; q < 5 * P + 5; ++q) {
+        // one voffset VGPR (lane + group); the slot and quad go in soffset
+        // (a constant) + the 12-bit immediate
+        const gw_u4 x = __builtin_amdgcn_raw_buffer_load_b128(g.r, (int)(g.base + lane * 16 + (q & 3) * 1024),
+                                                              (int)(off + (q >> 2) * 4096), 16);
+        W[4 * q + 0] = x.x;
+        W[4 * q + 1] = x.y;
+        W[4 * q + 2] = x.z;
+        W[4 * q + 3] = x.w;
+    }
+}
+
 __device__ __forceinline__ uint32_t total_blocks(uint32_t len) {
     // nfull data blocks + 1 padded block (+1 more when len % 64 >= 56)
     return (len >> 6) + (((len & 63u) < 56u) ? 1u : 2u);
@@ -242,6 +283,13 @@ __device__ __forceinline__ void produce_block(uint32_t k, uint32_t (&w)[16], uin
     SchedWrite<0, WK>::run(w, ring + ((m & 1u) * U + j) * kWBlockBytes, lane);
     // U == NPROD: each producer writes one block of every unit
     if (NPROD == 1 ? j == U - 1 : (U == NPROD || (k & 1u) == 1u)) split_barrier();
+}
+
+template <int U, bool WK, int NPROD = 1>
+__device__ __forceinline__ void produce_block_g(uint32_t k, uint32_t (&w)[16], const GRing& g, int lane) {
+    const uint32_t m = k / U, j = k - m * U;
+    SchedWriteG<0, WK>::run(w, g, ((m & 1u) * U + j) * kWBlockBytes, lane);
+    if (NPROD == 1 ? j == U - 1 : (U == NPROD || (k & 1u) == 1u)) gw_barrier();
 }
 
 
@@ -412,6 +460,27 @@ __device__ __forceinline__ void produce_stage_coop(const u32x4u* const (&src)[8]
     }
 }
 
+// kVGlobalW: the same, W+K to the global ring (the LDS slot still stages the
+// shared loads' transpose)
+template <int U, bool WK, int NPROD = 1>
+__device__ __forceinline__ void produce_stage_coop_g(const u32x4u* const (&src)[8], uint32_t s, uint32_t S,
+                                                     uint32_t (&cur)[32], uint8_t* ring, const GRing& g,
+                                                     uint32_t lane) {
+    const uint32_t k0 = 2 * s, m = k0 / U, j = k0 - m * U;
+    uint8_t* raw = ring + ((m & 1u) * U + j) * kWBlockBytes;
+    coop_store(raw, cur, lane);
+    if (s + 2 * NPROD < S) coop_load(src, s + 2 * NPROD, cur);
+    uint32_t x[32];
+    coop_read(raw, lane, x);
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+        uint32_t w[16];
+#pragma unroll
+        for (int q = 0; q < 16; ++q) w[q] = bswap(x[16 * half + q]);
+        produce_block_g<U, WK, NPROD>(k0 + half, w, g, (int)lane);
+    }
+}
+
 template <int U, bool WK, int NPROD>
 __device__ __forceinline__ void produce_own_block_coop(const u32x4u* const (&src)[4], uint32_t k, uint32_t K,
                                                        uint32_t (&cur)[16], uint8_t* ring, uint32_t lane) {
@@ -485,6 +554,12 @@ constexpr int kVRead20 = 4096;
 // the W slot): one load instruction touches 16 or 8 chunks instead of 64
 // (see `shared loads`).
 constexpr int kVCoop = 8192;
+// Round-2 A/B (A/B library only): the W+K ring in global memory (L2) instead
+// of LDS -- producers buffer-store it, the consumer buffer-loads it at device
+// scope (sc1: misses the CU's L1, hits the XCD's L2), with vmcnt(0) at the
+// barriers.  Tests whether a vector-memory load of the schedule costs the
+// consumer's issue stream less than a ds_read_b128 (~6 cycles).
+constexpr int kVGlobalW = 16384;
 template <int PAIRS, int V, int NPROD>
 constexpr int kSplitThreads = (V & kVLayout8) ? 512 : 64 * PAIRS * (1 + NPROD) + ((V & kVSkipWave2) ? 64 : 0);
 // Why W+K matters: the consumer's x = e + W + K as a VOP3 v_add3 (K in an
@@ -506,7 +581,7 @@ constexpr int kSplitNProd = U == 4 ? 2 : 1;
 template <int U, int J, int V, bool MASK>
 __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (&h)[5],
                                               const uint32_t (&Wc)[80], uint32_t (&Wn)[80],
-                                              const uint8_t* ring, int lane) {
+                                              const uint8_t* ring, const GRing& g, int lane) {
     // Block k+1 (k = k0 + J, k0 a multiple of 2U) is unit (k0/U + (J+1)/U),
     // whose parity is that of (J+1)/U since k0/U is even, and sub-block
     // (J+1) % U: the slot address is a compile-time offset.  A barrier goes
@@ -521,9 +596,27 @@ __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (
     } else {
         slot = ring + slot_idx * kWBlockBytes + lane * 16;
     }
-    if constexpr (jn == 0) split_barrier();
     uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
-    if constexpr ((V & kVRead20) != 0) {
+    if constexpr ((V & kVGlobalW) != 0) {
+        static_assert((V & (kVRtSlot | kVRead20)) == 0 && (V & kVRead10) != 0, "global W: the product's read order");
+        // this block's W (loaded during the previous block) in one wait, so
+        // hipcc adds none per quad
+        if constexpr (jn == 0)
+            gw_barrier();
+        else
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        constexpr uint32_t off = slot_idx * kWBlockBytes;
+        read_w_group_g<0>(g, off, lane, Wn);
+        read_w_group_g<1>(g, off, lane, Wn);
+        __builtin_amdgcn_sched_barrier(0);
+        RoundsW<0, 40, WK>::run(v, Wc);
+        __builtin_amdgcn_sched_barrier(0);
+        read_w_group_g<2>(g, off, lane, Wn);
+        read_w_group_g<3>(g, off, lane, Wn);
+        __builtin_amdgcn_sched_barrier(0);
+        RoundsW<40, 80, WK>::run(v, Wc);
+    } else if constexpr ((V & kVRead20) != 0) {
+        if constexpr (jn == 0) split_barrier();
         read_w_group<0>(slot, Wn);
         read_w_group<1>(slot, Wn);
         read_w_group<2>(slot, Wn);
@@ -531,6 +624,7 @@ __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (
         __builtin_amdgcn_sched_barrier(0);
         RoundsW<0, 80, WK>::run(v, Wc);
     } else if constexpr ((V & kVRead10) != 0) {
+        if constexpr (jn == 0) split_barrier();
         // two bursts of 10 reads (before rounds 0 and 40)
         read_w_group<0>(slot, Wn);
         read_w_group<1>(slot, Wn);
@@ -542,6 +636,7 @@ __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (
         __builtin_amdgcn_sched_barrier(0);
         RoundsW<40, 80, WK>::run(v, Wc);
     } else {
+        if constexpr (jn == 0) split_barrier();
         read_w_group<0>(slot, Wn);
         __builtin_amdgcn_sched_barrier(0);
         RoundsW<0, 20, WK>::run(v, Wc);
@@ -574,10 +669,10 @@ template <int U, int J, int V, bool MASK>
 struct ConsumeUnits {
     __device__ __forceinline__ static void run(uint32_t k0, uint32_t T, uint32_t (&h)[5],
                                                uint32_t (&Wa)[80], uint32_t (&Wb)[80],
-                                               const uint8_t* ring, int lane) {
+                                               const uint8_t* ring, const GRing& g, int lane) {
         if constexpr (J < 2 * U) {
-            consume_block<U, J, V, MASK>(k0 + J, T, h, Wa, Wb, ring, lane);
-            ConsumeUnits<U, J + 1, V, MASK>::run(k0, T, h, Wb, Wa, ring, lane);
+            consume_block<U, J, V, MASK>(k0 + J, T, h, Wa, Wb, ring, g, lane);
+            ConsumeUnits<U, J + 1, V, MASK>::run(k0, T, h, Wb, Wa, ring, g, lane);
         }
     }
 };
@@ -600,8 +695,11 @@ struct ConsumeUnits {
 // it on blockIdx.x, the mixed-batch kernel on the workgroups its plan gives
 // to this shape.
 template <int U, int PAIRS, int V, int NPROD>
-__device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uint32_t wg) {
+__device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uint32_t wg,
+                                           uint8_t* wring = nullptr) {
     constexpr bool WK = (V & kVWK) != 0;
+    constexpr bool GW = (V & kVGlobalW) != 0;
+    static_assert(!GW || (U == 4 && PAIRS == 1 && NPROD == 2 && (V & kVCoop) != 0), "global W: the config-2 shape");
     static_assert(PAIRS * 2 * U * kWBlockBytes <= 160 * 1024, "LDS");
     // Two producers for 2-block units (each owning one block per unit) were
     // measured slower at two groups per CU: 6 waves on 4 SIMDs put producers
@@ -630,6 +728,9 @@ __device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uin
     const int lane = threadIdx.x & 63;
     uint8_t* ring = lds + pair * (2 * U * kWBlockBytes);
     const uint32_t group = wg * PAIRS + (uint32_t)pair;
+    GRing g{};
+    if constexpr (GW) g = GRing{__builtin_amdgcn_make_buffer_rsrc(wring, 0, 0x7fffffff, 0x00020000),
+                                group * (2u * U * kWBlockBytes)};
     const uint32_t e = group * 64u + (uint32_t)lane;
     const bool valid = e < A.n;
     Entry en = fetch_entry(A, valid ? e : min(group * 64u, A.n - 1u));
@@ -705,13 +806,24 @@ __device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uin
             uint32_t C0[32], C1[32];
             if (pidx < S) coop_load(src, pidx, C0);
             if (pidx + NPROD < S) coop_load(src, pidx + NPROD, C1);
-            for (; s + NPROD < S; s += 2 * NPROD) {
-                produce_stage_coop<U, WK, NPROD>(src, s, S, C0, ring, (uint32_t)lane);
-                produce_stage_coop<U, WK, NPROD>(src, s + NPROD, S, C1, ring, (uint32_t)lane);
-            }
-            if (s < S) {
-                produce_stage_coop<U, WK, NPROD>(src, s, S, C0, ring, (uint32_t)lane);
-                s += NPROD;
+            if constexpr (GW) {
+                for (; s + NPROD < S; s += 2 * NPROD) {
+                    produce_stage_coop_g<U, WK, NPROD>(src, s, S, C0, ring, g, (uint32_t)lane);
+                    produce_stage_coop_g<U, WK, NPROD>(src, s + NPROD, S, C1, ring, g, (uint32_t)lane);
+                }
+                if (s < S) {
+                    produce_stage_coop_g<U, WK, NPROD>(src, s, S, C0, ring, g, (uint32_t)lane);
+                    s += NPROD;
+                }
+            } else {
+                for (; s + NPROD < S; s += 2 * NPROD) {
+                    produce_stage_coop<U, WK, NPROD>(src, s, S, C0, ring, (uint32_t)lane);
+                    produce_stage_coop<U, WK, NPROD>(src, s + NPROD, S, C1, ring, (uint32_t)lane);
+                }
+                if (s < S) {
+                    produce_stage_coop<U, WK, NPROD>(src, s, S, C0, ring, (uint32_t)lane);
+                    s += NPROD;
+                }
             }
         } else {
             Stage A0, A1;
@@ -734,31 +846,45 @@ __device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uin
                 const uint32_t k = 2 * s + half;
                 uint32_t w[16];
                 if (k < T) tail_block_words(en, k, w);
-                produce_block<U, WK, NPROD>(k, w, ring, lane);
+                if constexpr (GW)
+                    produce_block_g<U, WK, NPROD>(k, w, g, lane);
+                else
+                    produce_block<U, WK, NPROD>(k, w, ring, lane);
             }
         }
-        split_barrier();  // matches the consumer's last (unused) read
+        if constexpr (GW)
+            gw_barrier();
+        else
+            split_barrier();  // matches the consumer's last (unused) read
     } else {
         // ----------------------------- consumer -------------------------
         uint32_t h[5];
         load_init(A, en.id, h);
         uint32_t Wa[80], Wb[80];
         if constexpr ((V & kVPrio) != 0) __builtin_amdgcn_s_setprio(3);
-        split_barrier();  // B_0
-        read_w_group<0>(ring + lane * 16, Wa);
-        read_w_group<1>(ring + lane * 16, Wa);
-        read_w_group<2>(ring + lane * 16, Wa);
-        read_w_group<3>(ring + lane * 16, Wa);
+        if constexpr (GW) {
+            gw_barrier();  // B_0
+            read_w_group_g<0>(g, 0, lane, Wa);
+            read_w_group_g<1>(g, 0, lane, Wa);
+            read_w_group_g<2>(g, 0, lane, Wa);
+            read_w_group_g<3>(g, 0, lane, Wa);
+        } else {
+            split_barrier();  // B_0
+            read_w_group<0>(ring + lane * 16, Wa);
+            read_w_group<1>(ring + lane * 16, Wa);
+            read_w_group<2>(ring + lane * 16, Wa);
+            read_w_group<3>(ring + lane * 16, Wa);
+        }
         // Iterations in which every valid lane is still inside its chunk
         // commit without the per-lane select (all of them for equal lengths).
         const uint32_t Tmin = __builtin_amdgcn_readfirstlane(wave_min(valid ? T : 0xffffffffu));
         const uint32_t full = (V & kVUnmask) ? min(Tmin, units * U) / (2 * U) * (2 * U) : 0u;
         uint32_t k = 0;
         for (; k < full; k += 2 * U) {
-            ConsumeUnits<U, 0, V, false>::run(k, T, h, Wa, Wb, ring, lane);
+            ConsumeUnits<U, 0, V, false>::run(k, T, h, Wa, Wb, ring, g, lane);
         }
         for (; k < units * U; k += 2 * U) {
-            ConsumeUnits<U, 0, V, true>::run(k, T, h, Wa, Wb, ring, lane);
+            ConsumeUnits<U, 0, V, true>::run(k, T, h, Wa, Wb, ring, g, lane);
         }
         if (valid) emit(A, en.id, h);
     }
@@ -770,6 +896,16 @@ __global__ __launch_bounds__((kSplitThreads<PAIRS, V, NPROD>)) void sha1_split_k
     __shared__ __attribute__((aligned(16))) uint8_t lds[PAIRS * 2 * U * kWBlockBytes];
     split_body<U, PAIRS, V, NPROD>(A, lds, blockIdx.x);
 }
+
+#ifdef SHA1CHUNK_AB_VARIANTS
+// kVGlobalW A/B: the config-2 shape with its W+K ring in `wring` (groups x
+// 2 x U x 20 KiB of device memory)
+template <int V>
+__global__ __launch_bounds__((kSplitThreads<1, V, 2>)) void sha1_split_gw_kernel(BatchArgs A, uint8_t* wring) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[2 * 4 * kWBlockBytes];
+    split_body<4, 1, V, 2>(A, lds, blockIdx.x, wring);
+}
+#endif
 
 // --------------------------------------------------------------- fused ----
 // One wave, 64 chunks, schedule and rounds in registers (~630 VALU per
@@ -1335,7 +1471,7 @@ bool split_unit_built(int u) {
 #ifdef SHA1CHUNK_AB_VARIANTS
     static const int built[] = {1,  2,  3,  4,  8,  9,  10, 11, 12, 20, 21, 22, 23, 24, 26, 27,
                                 30, 31, 32, 33, 34, 36, 37, 42, 44, 45, 46, 504, 505, 506, 507,
-                                569, 577, 578, 579, 580, 581, 13, 583, 584, 585, 86, 87};
+                                569, 577, 578, 579, 580, 581, 13, 583, 584, 585, 86, 87, 590};
     for (int b : built)
         if (u == b) return true;
     return false;
@@ -1424,6 +1560,22 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     case 8:  // 4 pairs per workgroup (512 threads), one consumer + producer per SIMD
         hipLaunchKernelGGL((sha1_split_kernel<1, 4>), dim3((groups + 3) / 4), dim3(512), 0, st, A);
         break;
+    case 590: {  // the product's case 4 with the W+K ring in global memory (kVGlobalW)
+        static uint8_t* wring = nullptr;
+        static size_t wcap = 0;
+        const size_t need = (size_t)groups * 2 * 4 * kWBlockBytes;
+        if (need > 0x7fffffffu) return hipErrorInvalidValue;
+        if (need > wcap) {
+            if (wring) (void)hipFree(wring);
+            wring = nullptr;
+            wcap = 0;
+            hipError_t e = hipMalloc(&wring, need);
+            if (e != hipSuccess) return e;
+            wcap = need;
+        }
+        hipLaunchKernelGGL((sha1_split_gw_kernel<kSplitV<4> | kVGlobalW>), dim3(groups), dim3(256), 0, st, A, wring);
+        break;
+    }
     case 86:  // case 8 with shared producer loads (4 groups per CU, A/B vs fused)
         hipLaunchKernelGGL((sha1_split_kernel<1, 4, kVWK | kVUnmask | kVCoop>), dim3((groups + 3) / 4), dim3(512),
                            0, st, A);
