@@ -31,7 +31,7 @@ hipError_t launch_fused(const BatchArgs& A, hipStream_t st);
 // (4-block units, two producers: <= 1 group per CU), 11 (8-wave workgroup of
 // two pairs: <= 2 groups per CU).  The A/B library (`make ab`,
 // -DSHA1CHUNK_AB_VARIANTS) also builds the study's other shapes and variant
-// flags (2, 3, 8-10, 12, 10*U+V, 500+V, 569, 577, 578).
+// flags (2, 3, 8-10, 12, 13, 10*U+V, 500+V, 569, 577-585, 86, 87, 590).
 bool split_unit_built(int unit_blocks);
 hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st);
 // Sorted ragged batch of more groups than CUs (A.order set, sorted_len =
