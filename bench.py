@@ -24,6 +24,20 @@ host's cores on the same chunks).
 --streams P (default 1) keeps P independent batches in flight on P HIP
 streams (each its own 4096 distinct chunks); the default measures one batch
 at a time.
+
+`strong` (same JSON line): BASELINE config 4 -- the fixed list of 262144 x
+512 KiB chunks split into N contiguous shards, one per rank (shard.strong_shard,
+no collective) -- timed like the main leg (barrier + synchronize around K
+steps, max over ranks), with its speed-up and efficiency against the one-GPU
+time of the whole 262144-chunk list, measured on rank 0's GPU in the same run
+(at N = 1 the shard is the whole list).  Parity: every rank's digest-of-digests
+against the reference golden shard aggregate of the N-way split.
+`value` stays the weak config-2 number, so the N = 1 line is BENCH's.
+
+`latency_one_chunk` (N = 1): the peer's synchronous receive-side verify,
+verify_hash() (job.c:217-228) on one 512 KiB chunk through the library, in a
+child process: cold (first call, HIP start-up included) and warm, next to the
+reference sha.c -O2 on one host core (cpu_baseline leg).
 """
 from __future__ import annotations
 
@@ -78,13 +92,22 @@ NAMED_WORKLOADS = {4096: "BASELINE config 2", 32768: "config 4 shard, 1 of 8 GPU
 
 def _regime(n: int, cus: int, kernel: str) -> str:
     """The kernel `kernel` (or AUTO's choice, sha1_runtime.hip choose_kernel /
-    split_unit) for n chunks on `cus` CUs."""
+    split_unit) for n chunks on `cus` CUs, honouring the same A/B overrides
+    the library reads (SHA1CHUNK_FORCE_KERNEL behind AUTO,
+    SHA1CHUNK_SPLIT_UNIT for the split shape)."""
     groups = (n + 63) // 64
     if kernel == "auto":
-        kernel = "split" if groups <= 2 * cus else "fused"
+        forced = os.environ.get("SHA1CHUNK_FORCE_KERNEL")
+        if forced in ("lane", "fused", "split"):
+            kernel = forced
+        else:
+            kernel = "split" if groups <= 2 * cus else "fused"
     if kernel == "split":
-        return "split_u4_2prod" if groups <= cus else ("split_u2_8wave" if groups <= 2 * cus
-                                                        else "split_u1")
+        unit = os.environ.get("SHA1CHUNK_SPLIT_UNIT")
+        if unit is None:
+            unit = "4" if groups <= cus else ("11" if groups <= 2 * cus else "1")
+        return {"4": "split_u4_2prod", "11": "split_u2_8wave", "1": "split_u1"}.get(
+            unit.strip(), f"split_unit{unit.strip()}")
     return kernel
 
 
@@ -99,6 +122,10 @@ def parse():
     ap.add_argument("--streams", type=int, default=1, help="independent batches in flight")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--strong-total", type=int, default=262144,
+                    help="chunks of the strong-scaling list (BASELINE config 4); 0 = skip")
+    ap.add_argument("--strong-steps", type=int, default=5)
+    ap.add_argument("--no-latency", action="store_true")
     return ap.parse_args()
 
 
@@ -194,7 +221,7 @@ def main():
     # VALU ceiling of the chip for SHA-1 (every SIMD busy with the fused
     # kernel's op mix at the max clock), in the same GB/s as the roofline
     valu_peak = cus * SIMDS_PER_CU * 64 * 64 / FUSED_SIMD_CYCLES_PER_BLOCK * CLOCK_HZ / 1e9
-    if regime.startswith("split"):
+    if regime in ("split_u4_2prod", "split_u2_8wave"):
         floor_ms = blocks * CONSUMER_INSTR_PER_BLOCK * ISSUE_CYCLES / CLOCK_HZ * 1e3
         binding = {
             "limit": "per-chunk serial instruction issue (SHA-1 is serial inside a chunk; "
@@ -218,7 +245,7 @@ def main():
                      "221.75 full-rate x 2 per block, profiles/isa_mix_r02.json); the chip "
                      "holds ~2.05 GHz under this load (profiles/pmc_fused_131072_r01.json)",
         }
-    else:  # forced lane kernel (per-lane loads, A/B and test path): not modelled
+    else:  # forced lane kernel, 1-block or A/B split shapes: not modelled
         binding = {"limit": "not modelled", "kernel": regime, "achieved_ms": round(kern_ms, 4)}
     label = f"{n} x {L} B chunks per GPU, device-resident"
     if L == CHUNK_LEN and n in NAMED_WORKLOADS:
@@ -238,7 +265,8 @@ def main():
         "dtype": "u32",
         "data": "synthetic (splitmix64 corpus, SURVEY.md 8d), resident in HBM",
         "config": {"workload": label,
-                   "chunks_per_gpu": n, "chunk_bytes": L, "kernel": regime, "streams": P,
+                   "chunks_per_gpu": n, "chunk_bytes": L, "kernel": regime,
+                   "kernel_requested": a.kernel, "streams": P,
                    "parallelism": f"chunk-sharded x{world}, no collective"},
         "parity": parity,
         # HBM is the metric's denominator (BASELINE.json), not the binding
@@ -262,13 +290,129 @@ def main():
         },
         "binding_limit": binding,
     }
+    # free the config-2 buffers before the strong leg's 128 GiB / N
+    del bufs, digs
+    torch.cuda.empty_cache()
+    if a.strong_total > 0:
+        result["strong"] = _strong_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden)
+    if rank == 0 and world == 1 and not a.no_latency:
+        result["latency_one_chunk"] = _latency_one_chunk(dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         from oracle import oracle as O  # the CPU baseline leg only: the reference sha.c, timed
         result["cpu_baseline"] = _cpu_baseline(O, n, L, a.cpu_threads, golden)
+        if "latency_one_chunk" in result:
+            result["latency_one_chunk"]["reference_sha_c_one_core_ms"] = \
+                result["cpu_baseline"].pop("one_chunk_ms")
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _time_launches(pkg, torch, buf, L, n, dig, stream, steps, warmup):
+    """warmup untimed launches, then `steps` launches bracketed by
+    synchronize: (wall seconds, mean HIP-event ms per launch)."""
+    for _ in range(warmup):
+        pkg.hash_uniform_device(buf, L, n, dig, stream=stream)
+    torch.cuda.synchronize()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(stream)
+        pkg.hash_uniform_device(buf, L, n, dig, stream=stream)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    return time.perf_counter() - t0, float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
+
+
+def _strong_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden):
+    """BASELINE config 4 strong scaling: the fixed list of `total` chunks
+    split into `world` contiguous shards (no collective on the data path)."""
+    total, L, K = a.strong_total, CHUNK_LEN, max(1, a.strong_steps)
+    first, cnt = shard.strong_shard(rank, world, total)
+    st = torch.cuda.Stream()
+    buf = torch.empty(max(cnt, 1) * L, dtype=torch.uint8, device="cuda")
+    dig = torch.zeros((max(cnt, 1), 20), dtype=torch.uint8, device="cuda")
+    pkg.synth_fill_device(buf, first, cnt, L, stream=st)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall, kern_ms = _time_launches(pkg, torch, buf, L, cnt, dig, st, K, 1)
+    if world > 1:
+        dist.barrier()
+    wall, kern_ms = shard.max_over_ranks([wall, kern_ms], device=cdev)
+    got = dig[:cnt].cpu().numpy()
+    aggs = golden["config4"]["shard_aggs"].get(str(world)) if total == golden["config4"]["chunks"] \
+        else None
+    ok = aggs is not None and hashlib.sha1(got.tobytes()).hexdigest() == aggs[rank]
+    parity = shard.all_ranks_ok(ok, device=cdev)
+    del buf, dig
+    torch.cuda.empty_cache()
+    ms_n = wall / K * 1e3
+    # the one-GPU time of the whole list: at N = 1 that is this leg; at N > 1
+    # rank 0 hashes all `total` chunks on its own GPU while the others wait
+    one_ms, one_kern_ms, one_parity = ms_n, kern_ms, parity
+    if world > 1:
+        if rank == 0:
+            buf = torch.empty(total * L, dtype=torch.uint8, device="cuda")
+            dig = torch.zeros((total, 20), dtype=torch.uint8, device="cuda")
+            pkg.synth_fill_device(buf, 0, total, L, stream=st)
+            torch.cuda.synchronize()
+            w1, one_kern_ms = _time_launches(pkg, torch, buf, L, total, dig, st, K, 1)
+            one_ms = w1 / K * 1e3
+            one_parity = hashlib.sha1(dig.cpu().numpy().tobytes()).hexdigest() == \
+                golden["config4"]["agg"]
+            del buf, dig
+            torch.cuda.empty_cache()
+        dist.barrier()
+    return shard.strong_report(total, L, world, ms_n, kern_ms, one_ms, one_kern_ms, parity,
+                               one_parity, K)
+
+
+def _latency_one_chunk(dev: int) -> dict:
+    """verify_hash (job.c:217-228) on one 512 KiB chunk through the library in
+    a child process: the first call (HIP start-up and stream creation
+    included) and the median of 20 warm calls."""
+    import subprocess
+    code = (
+        "import ctypes, hashlib, json, os, sys, time\n"
+        "import numpy as np\n"
+        "L = 524288\n"
+        "data = np.random.default_rng(5).integers(0, 256, L, dtype=np.uint8).tobytes()\n"
+        "hexd = hashlib.sha1(data).hexdigest().encode()\n"
+        "t0 = time.perf_counter()\n"
+        "lib = ctypes.CDLL(sys.argv[1])\n"
+        "lib.verify_hash.argtypes = [ctypes.c_char_p, ctypes.c_char_p]\n"
+        "lib.sha1chunk_set_device(int(sys.argv[2]))\n"
+        "t1 = time.perf_counter()\n"
+        "assert lib.verify_hash(hexd, data) == 0\n"
+        "t2 = time.perf_counter()\n"
+        "warm = []\n"
+        "for _ in range(20):\n"
+        "    a = time.perf_counter(); r = lib.verify_hash(hexd, data); warm.append(time.perf_counter() - a)\n"
+        "    assert r == 0\n"
+        "bad = bytes(data[:7]) + bytes([data[7] ^ 1]) + bytes(data[8:])\n"
+        "assert lib.verify_hash(hexd, bad) == 1\n"
+        "sys.stdout.flush()\n"
+        "print('LATENCY ' + json.dumps({'probe_ms': (t1 - t0) * 1e3, 'first_call_ms': (t2 - t1) * 1e3,\n"
+        "      'warm_ms': float(np.median(warm)) * 1e3, 'warm_min_ms': min(warm) * 1e3}))\n")
+    libp = os.path.join(ROOT, "congestion-control-with-bittorren_amd", "libsha1chunk.so")
+    try:
+        r = subprocess.run([sys.executable, "-c", code, libp, str(dev)], capture_output=True,
+                           text=True, timeout=120)
+        line = [x for x in r.stdout.splitlines() if x.startswith("LATENCY ")]
+        if r.returncode != 0 or not line:
+            return {"error": (r.stderr or r.stdout)[-300:]}
+        d = json.loads(line[-1][8:])
+    except Exception as e:  # a failed probe must not cost the bench line
+        return {"error": repr(e)[:300]}
+    return {"path": "verify_hash -> get_chunk_hash -> shahash -> sha1chunk_hash_batch(n=1): "
+                    "one lane of the split kernel (job.c:217-228)",
+            "cold_ms": round(d["probe_ms"] + d["first_call_ms"], 3),
+            "cold_first_call_ms": round(d["first_call_ms"], 3),
+            "warm_ms": round(d["warm_ms"], 3), "warm_min_ms": round(d["warm_min_ms"], 3),
+            "bytes": CHUNK_LEN}
 
 
 def _traffic(n: int, L: int):
@@ -300,7 +444,11 @@ def _cpu_baseline(O, n, L, threads, golden, min_cpu_seconds=12.0, max_passes=8):
             ok = agg.hex() == golden["weak4096"][0]
             same = ok if same is None else (same and ok)
     secs = float(np.median(times))
+    # the peer's per-chunk verify on the CPU: one 512 KiB chunk on one core
+    # (median of 16 single-chunk passes of the same reference build)
+    one = [O.time_synth(1, L, threads=1, first=i, kind=kind)[0] for i in range(16)]
     return {"value": round(sample * L / secs / 2**30, 3), "unit": "GiB/s", "cores": threads,
+            "one_chunk_ms": round(float(np.median(one)) * 1e3, 3),
             "kind": kind,
             "sample": f"chunks 0..{sample - 1} x {L} B of the same corpus, -O2, {threads} pthreads "
                       f"chunk-strided, median of {len(times)} passes ({sum(times) * threads:.1f} "

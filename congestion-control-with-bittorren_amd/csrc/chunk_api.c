@@ -22,6 +22,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <sys/stat.h>
+#include <time.h>
 #include <unistd.h>
 
 #include "../../include/chunk_hash.h"
@@ -199,14 +200,20 @@ char *get_chunk_hash(char *chunk, size_t size) {
  * the second verify against one file on, a single streamed device pass
  * digests all of its chunks -- each zero-padded to CHUNK_LEN, exactly what
  * this verify hashes -- and later requests are a table lookup.  The table is
- * keyed on (st_dev, st_ino, st_size, st_mtim) and rebuilt when any of them
- * changes; non-regular files and SHA1CHUNK_MASTER_INDEX=0 keep the per-call
- * path. */
+ * keyed on (st_dev, st_ino, st_size, st_mtim, st_ctim) and rebuilt when any
+ * of them changes.  st_ctim moves on every write and on every utime(), so an
+ * in-place rewrite that keeps the size and restores the mtime is caught.  A
+ * write landing in the same timestamp tick as the keyed one would not be, so
+ * a file whose ctime is less than SHA1CHUNK_MASTER_SETTLE_MS (default 2000)
+ * old is never served from the table: it is re-read and re-hashed per call,
+ * as the reference does (chunk.c:204-217).  Non-regular files and
+ * SHA1CHUNK_MASTER_INDEX=0 keep the per-call path. */
 typedef struct {
     dev_t dev;
     ino_t ino;
     off_t size;
     struct timespec mtime;
+    struct timespec ctime;
 } file_key;
 
 static struct {
@@ -255,7 +262,20 @@ static void index_sink(void *ctx, size_t first, const uint8_t *dig, size_t count
 
 static int same_key(const file_key *a, const file_key *b) {
     return a->dev == b->dev && a->ino == b->ino && a->size == b->size &&
-           a->mtime.tv_sec == b->mtime.tv_sec && a->mtime.tv_nsec == b->mtime.tv_nsec;
+           a->mtime.tv_sec == b->mtime.tv_sec && a->mtime.tv_nsec == b->mtime.tv_nsec &&
+           a->ctime.tv_sec == b->ctime.tv_sec && a->ctime.tv_nsec == b->ctime.tv_nsec;
+}
+
+/* 1 when the file's last change (ctime) is older than the settle time. */
+static int settled(const struct stat *st) {
+    const char *env = getenv("SHA1CHUNK_MASTER_SETTLE_MS");
+    const long long settle_ms = env ? atoll(env) : 2000;
+    struct timespec now;
+    if (settle_ms <= 0) return 1;
+    if (clock_gettime(CLOCK_REALTIME, &now)) return 0;
+    const long long age_ms = (long long)(now.tv_sec - st->st_ctim.tv_sec) * 1000 +
+                             (now.tv_nsec - st->st_ctim.tv_nsec) / 1000000;
+    return age_ms >= settle_ms;
 }
 
 /* Copies chunk `idx`'s digest from the index into out20 and the file size
@@ -266,7 +286,8 @@ static int master_lookup(FILE *f, size_t idx, uint8_t out20[20], off_t *size) {
     struct stat st;
     int fd = fileno(f);
     if (fd < 0 || fstat(fd, &st) || !S_ISREG(st.st_mode) || st.st_size <= 0) return 0;
-    file_key k = {st.st_dev, st.st_ino, st.st_size, st.st_mtim};
+    if (!settled(&st)) return 0; /* changed just now: re-read and re-hash */
+    file_key k = {st.st_dev, st.st_ino, st.st_size, st.st_mtim, st.st_ctim};
     int hit = 0;
     pthread_mutex_lock(&master.mu);
     if (!same_key(&k, &master.key)) {

@@ -335,6 +335,16 @@ __device__ __forceinline__ void load_stage(const uint8_t* p, Stage& st) {
 constexpr uint32_t kCoopStageBytes = 64u * 128u;
 constexpr uint32_t kCoopWaveBytes = 2u * kCoopStageBytes;
 
+// Orders one wave's LDS accesses across a transpose: lane-to-lane exchange
+// through LDS (coop_store -> coop_read, and the reads of a buffer before its
+// next stores).  The hardware completes a wave's LDS ops in order; this pins
+// the program order in the compiler too (a wavefront-scope fence and the
+// wave barrier pseudo-op: neither emits an instruction).
+__device__ __forceinline__ void wave_lds_order() {
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+}
+
 __device__ __forceinline__ uint32_t coop_slot(uint32_t c, uint32_t piece) {
     return c * 128u + ((piece + (c >> 1)) & 7u) * 16u;
 }
@@ -450,7 +460,9 @@ __device__ __forceinline__ void produce_stage_coop(const u32x4u* const (&src)[8]
     coop_store(raw, cur, lane);
     if (s + 2 * NPROD < S) coop_load(src, s + 2 * NPROD, cur);
     uint32_t x[32];
+    wave_lds_order();
     coop_read(raw, lane, x);
+    wave_lds_order();  // the W writes below overwrite what was just read
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
         uint32_t w[16];
@@ -471,7 +483,9 @@ __device__ __forceinline__ void produce_stage_coop_g(const u32x4u* const (&src)[
     coop_store(raw, cur, lane);
     if (s + 2 * NPROD < S) coop_load(src, s + 2 * NPROD, cur);
     uint32_t x[32];
+    wave_lds_order();
     coop_read(raw, lane, x);
+    wave_lds_order();  // the W writes below overwrite what was just read
 #pragma unroll
     for (int half = 0; half < 2; ++half) {
         uint32_t w[16];
@@ -489,7 +503,9 @@ __device__ __forceinline__ void produce_own_block_coop(const u32x4u* const (&src
     coop4_store(raw, cur, lane);
     if (k + 2 * NPROD < K) coop4_load(src, k + 2 * NPROD, cur);
     uint32_t w[16];
+    wave_lds_order();
     coop4_read(raw, lane, w);
+    wave_lds_order();  // the W writes below overwrite what was just read
 #pragma unroll
     for (int q = 0; q < 16; ++q) w[q] = bswap(w[q]);
     produce_block<U, WK, NPROD>(k, w, ring, (int)lane);
@@ -1066,7 +1082,9 @@ __device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, 
         coop_load(src, min(1u, S - 1u), v);
         for (uint32_t s = 0; s < S; ++s) {
             uint32_t cur[32];
+            wave_lds_order();  // stage s stored (previous iteration) -> read
             coop_read(lds + (s & 1u) * kCoopStageBytes, lane, cur);
+            wave_lds_order();  // buffer (s+1)&1 was read last iteration -> store
             coop_store(lds + ((s + 1u) & 1u) * kCoopStageBytes, v, lane);
             coop_load(src, min(s + 2u, S - 1u), v);
             coop_compress<RV>(cur, h);
@@ -1357,8 +1375,11 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         add(0, hb, fb);
         add(1, 0, 0);
         add(0, G, 4);
+        // heads below the bounds' best; only H <= hcap (prefix[] holds P_H
+        // there) -- when the best is all-split beyond hcap, hb - d would be
+        // neither a searched head nor all-split
         for (uint32_t d = 1; d <= 64; d *= 2) {
-            if (hb >= d) add(0, hb - d, fb);
+            if (hb >= d && hb - d <= hcap) add(0, hb - d, fb);
             if (hb + d <= hcap) add(0, hb + d, fb);
         }
         const uint32_t top = min(hcap, 2u * cus);

@@ -291,13 +291,21 @@ hipError_t launch(int kernel, const BatchArgs& A, int cus, hipStream_t st) {
     }
 }
 
-int launch_checked(int kernel, const BatchArgs& A, hipStream_t st, int cus = 256) {
-    if (kernel < SHA1CHUNK_KERNEL_LANE || kernel > SHA1CHUNK_KERNEL_SPLIT)
-        return fail(SHA1CHUNK_EINVAL, "unknown kernel id %d", kernel);
-    if (A.n > 0xffffffffu - 1024u)  // grid sizes are computed in 32 bits
+// Checks every launch path shares (plain kernels and the mixed kernel):
+// grid sizes are computed in 32 bits ((n + 255) / 256, (n + 63) / 64), and
+// digests are stored as 32-bit words.
+int check_batch(const BatchArgs& A) {
+    if (A.n > 0xffffffffu - 1024u)
         return fail(SHA1CHUNK_EINVAL, "batch of %u chunks: at most 2^32 - 1025 per call", A.n);
     if (A.n > 0 && (reinterpret_cast<uintptr_t>(A.dig) & 3u))
         return fail(SHA1CHUNK_EALIGN, "digest buffer must be 4-byte aligned");
+    return SHA1CHUNK_OK;
+}
+
+int launch_checked(int kernel, const BatchArgs& A, hipStream_t st, int cus = 256) {
+    if (kernel < SHA1CHUNK_KERNEL_LANE || kernel > SHA1CHUNK_KERNEL_SPLIT)
+        return fail(SHA1CHUNK_EINVAL, "unknown kernel id %d", kernel);
+    if (int rc = check_batch(A)) return rc;
     if (kernel == SHA1CHUNK_KERNEL_SPLIT && !split_unit_built(split_unit(A.n, cus)))
         return fail(SHA1CHUNK_EINVAL, "split shape %d is not in this library (A/B shapes: `make ab`)",
                     split_unit(A.n, cus));
@@ -322,8 +330,7 @@ bool use_mixed() {
 // diagnostics only).
 int launch_mixed_checked(const BatchArgs& A, const uint32_t* sorted_len, uint32_t* plan, int cus,
                          hipStream_t st) {
-    if (A.n > 0 && (reinterpret_cast<uintptr_t>(A.dig) & 3u))
-        return fail(SHA1CHUNK_EALIGN, "digest buffer must be 4-byte aligned");
+    if (int rc = check_batch(A)) return rc;
     int forced[3] = {0, 0, 0};
     bool force = false;
     if (const char* e = getenv("SHA1CHUNK_MIXED_PLAN")) {
@@ -361,7 +368,11 @@ int launch_mixed_checked(const BatchArgs& A, const uint32_t* sorted_len, uint32_
 // Slot size scales with the batch: a pass of the kernel takes ~7 ms however
 // few chunks it has (serial per chunk), so a slot must carry enough bytes
 // that its PCIe copy, not the kernel, is the longer stage.
+// SHA1CHUNK_HOST_SLOT_MIB (16..1024, read per call) fixes the slot size, so
+// tests can wrap the two-slot ring many times over a modest batch.
 size_t slot_bytes_for(uint64_t total) {
+    if (const char* e = getenv("SHA1CHUNK_HOST_SLOT_MIB"))
+        return std::min<size_t>(1024, std::max<size_t>(16, atoi(e))) << 20;
     const size_t lo = size_t(256) << 20, hi = size_t(1) << 30;
     return std::min(hi, std::max(lo, static_cast<size_t>(total / 4)));
 }
@@ -424,6 +435,12 @@ int stage_and_launch(Device& D, Slot& s, const uint8_t* base, const uint64_t* of
         span += lengths[id];
     }
     const size_t dbytes = direct ? round_up(span, kAlign) : data_bytes;
+    // SHA1CHUNK_HOST_DEBUG=1: one line per slot fill (tests check the mode
+    // and the number of ring wraps; diagnostics only)
+    if (const char* dbg = getenv("SHA1CHUNK_HOST_DEBUG"); dbg && atoi(dbg))
+        fprintf(stderr, "sha1chunk host slot %d: %zu chunks %zu bytes %s\n",
+                static_cast<int>(&s - D.slot), m, direct ? static_cast<size_t>(span) : data_bytes,
+                direct ? "direct" : "packed");
     if ((rc = s.hpin.ensure(meta + (direct ? 0 : data_bytes))) || (rc = s.dmem.ensure(meta + dbytes)) ||
         (rc = s.hdig.ensure(m * 20)) || (rc = s.ddig.ensure(m * 20)))
         return rc;
@@ -622,6 +639,7 @@ int sha1chunk_hash_device_async(const void* d_base, const uint64_t* d_offsets,
     // AUTO on a ragged batch: hash longest-first (sha1_sort.hip); with more
     // groups of 64 than CUs, through the mixed kernel and its device-side
     // plan (sha1_kernels.hip, mixed).
+    if ((rc = check_batch(A))) return rc;
     void* scratch = nullptr;
     if (kernel == SHA1CHUNK_KERNEL_AUTO && n > 64) {
         const uint32_t* sorted_len = nullptr;

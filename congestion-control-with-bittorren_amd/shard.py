@@ -26,6 +26,29 @@ def strong_shard(rank: int, world: int, total: int) -> tuple[int, int]:
     return first, base + (1 if rank < extra else 0)
 
 
+def strong_report(total: int, chunk_len: int, world: int, ms_n: float, kern_ms_n: float,
+                  ms_1: float, kern_ms_1: float, parity: bool, parity_1: bool,
+                  steps: int) -> dict:
+    """The `strong` object of bench.py's JSON line: `total` chunks split over
+    `world` GPUs took ms_n per step (max over ranks), the whole list on one
+    GPU ms_1.  GiB/s counts every chunk byte of the list; speed-up and
+    efficiency are against the one-GPU time."""
+    speedup = ms_1 / ms_n if ms_n > 0 else 0.0
+    return {
+        "workload": f"BASELINE config 4: {total} x {chunk_len} B chunks split over {world} GPU(s), "
+                    "device-resident",
+        "chunks_total": total, "chunks_per_gpu": -(-total // world) if world else total,
+        "n_gpus": world, "steps": steps,
+        "ms_per_step": round(ms_n, 4), "kernel_ms": round(kern_ms_n, 4),
+        "value": round(total * chunk_len / (ms_n * 1e-3) / 2**30, 3) if ms_n > 0 else 0.0,
+        "unit": "GiB/s",
+        "one_gpu_ms_per_step": round(ms_1, 4), "one_gpu_kernel_ms": round(kern_ms_1, 4),
+        "speedup": round(speedup, 4), "efficiency": round(speedup / world, 4) if world else 0.0,
+        "parity": bool(parity), "one_gpu_parity": bool(parity_1),
+        "scaling": "strong",
+    }
+
+
 def byte_balanced_cuts(lengths, world: int) -> list[int]:
     """Cut points (len world+1) splitting a ragged chunk list into contiguous
     slices of near-equal byte counts (what SHA1CHUNK_ALL_DEVICES does in

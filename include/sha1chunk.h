@@ -68,8 +68,12 @@ int sha1chunk_verify_batch(const void *base, const uint64_t *offsets, const uint
 
 /* Device-resident, asynchronous on `stream` (a hipStream_t, NULL = default).
  * All pointers are device pointers.  Returns after enqueueing.  Chunks may
- * start at any byte and lie anywhere in the buffer (16-byte aligned starts
- * are ~10 % faster in the fused shapes; placement costs nothing). */
+ * start at any byte and lie anywhere in the buffer.  With KERNEL_AUTO (the
+ * split shapes and the mixed kernel, whose loads are shared across the
+ * wave) placement costs nothing and 16-byte aligned starts are ~10 % faster
+ * in the fused shapes.  A forced KERNEL_FUSED or KERNEL_LANE loads one chunk
+ * per lane and is layout-sensitive: chunks scattered far apart thrash the
+ * address-translation cache (~2.8x slower measured). */
 int sha1chunk_hash_device_async(const void *d_base, const uint64_t *d_offsets,
                                 const uint32_t *d_lengths, size_t n, uint8_t *d_digests,
                                 void *stream, int kernel);

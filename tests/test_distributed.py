@@ -72,6 +72,42 @@ def test_two_rank_weak_sharding(tmp_path, oracle):
     assert not np.array_equal(d0, d1)
 
 
+def _strong_worker(rank, world, port, out_dir):
+    """bench.py's strong leg control plane: each rank takes its contiguous
+    config-4 shard, the per-rank times are max-reduced, parity is ANDed, and
+    shard.strong_report builds the JSON object."""
+    import importlib
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    shard = importlib.import_module("congestion-control-with-bittorren_amd.shard")
+    first, cnt = shard.strong_shard(rank, world, 262144)
+    wall, kern = shard.max_over_ranks([0.030 + 0.001 * rank, 6.0 + rank])
+    parity = shard.all_ranks_ok(True)
+    rep = shard.strong_report(262144, 524288, world, wall / 5 * 1e3, kern, 39.5, 39.3, parity, True, 5)
+    np.save(os.path.join(out_dir, f"s{rank}.npy"),
+            np.array([first, cnt, rep["ms_per_step"], rep["kernel_ms"], rep["speedup"],
+                      rep["efficiency"], rep["value"], rep["parity"]], dtype=np.float64))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_rank_strong_leg_control_plane(tmp_path):
+    world = 2
+    mp.start_processes(_strong_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world,
+                       join=True, start_method="spawn")
+    s0, s1 = np.load(tmp_path / "s0.npy"), np.load(tmp_path / "s1.npy")
+    assert (s0[0], s0[1], s1[0], s1[1]) == (0, 131072, 131072, 131072)
+    assert np.array_equal(s0[2:], s1[2:])  # every rank reports the same maxima
+    assert s0[2] == pytest.approx(31 / 5) and s0[3] == 7.0
+    assert s0[4] == pytest.approx(39.5 / (31 / 5), rel=1e-3)
+    assert s0[5] == pytest.approx(s0[4] / 2, rel=1e-3)
+    assert s0[6] == pytest.approx(262144 * 524288 / (31 / 5 * 1e-3) / 2**30, rel=1e-3)
+    assert s0[7] == 1.0
+
+
 def test_strong_and_byte_balanced_shards(pkg):
     shard = pkg.shard if hasattr(pkg, "shard") else __import__(
         "importlib").import_module("congestion-control-with-bittorren_amd.shard")

@@ -103,7 +103,7 @@ def candidates(G, C, hcap, hb, fb):
     add(0, G, 4)
     d = 1
     while d <= 64:
-        if hb >= d:
+        if hb >= d and hb - d <= hcap:
             add(0, hb - d, fb)
         if hb + d <= hcap:
             add(0, hb + d, fb)

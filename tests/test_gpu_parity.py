@@ -567,12 +567,37 @@ def test_verify_queue_full_batches_drain_by_polling(pkg, dev, monkeypatch, grow)
 _VERIFY_DRIVER = r'''
 #include <stdio.h>
 #include <stdlib.h>
+#include <string.h>
+#include <sys/stat.h>
+#include <fcntl.h>
+#include <unistd.h>
 #include "chunk_hash.h"
-/* argv: file idx hex [idx hex ...] -> verify_chunk_hash each pair in order */
+/* argv: file idx hex [idx hex ...] -> verify_chunk_hash each pair in order;
+ * the pair "W src" instead rewrites the file in place with src's bytes (same
+ * size) and puts its old atime/mtime back, as a copy tool preserving times
+ * would */
+static void rewrite_keep_mtime(const char *dst, const char *src) {
+    struct stat st;
+    static char buf[1 << 20];
+    int in = open(src, O_RDONLY), out = open(dst, O_WRONLY);
+    if (in < 0 || out < 0 || fstat(out, &st)) exit(3);
+    ssize_t n;
+    while ((n = read(in, buf, sizeof buf)) > 0)
+        if (write(out, buf, (size_t)n) != n) exit(3);
+    struct timespec t[2] = {st.st_atim, st.st_mtim};
+    if (futimens(out, t)) exit(3);
+    close(in);
+    close(out);
+}
 int main(int argc, char **argv) {
     FILE *f = fopen(argv[1], "r");
     if (!f) return 2;
     for (int i = 2; i + 1 < argc; i += 2) {
+        if (!strcmp(argv[i], "W")) {
+            rewrite_keep_mtime(argv[1], argv[i + 1]);
+            printf("rewrote\n");
+            continue;
+        }
         verify_chunk_hash(f, argv[i + 1], (size_t)atoll(argv[i]));
         printf("ok %s pos %ld\n", argv[i], ftell(f));
     }
@@ -593,8 +618,11 @@ def verify_driver(tmp_path_factory):
     return str(exe)
 
 
-def _run_verify(exe, path, pairs, index=True):
-    env = dict(os.environ, SHA1CHUNK_MASTER_INDEX="1" if index else "0")
+def _run_verify(exe, path, pairs, index=True, settle_ms="0"):
+    # settle 0: the index serves files changed just now too (the tests write
+    # their master files a moment before the driver starts)
+    env = dict(os.environ, SHA1CHUNK_MASTER_INDEX="1" if index else "0",
+               SHA1CHUNK_MASTER_SETTLE_MS=settle_ms)
     args = [exe, path] + [x for i, h in pairs for x in (str(i), h)]
     return subprocess.run(args, capture_output=True, text=True, env=env)
 
@@ -647,6 +675,38 @@ def test_verify_chunk_hash_ragged_master_and_mismatch(pkg, dev, oracle, verify_d
     new1 = hashlib.sha1(bytes(data2[L512:2 * L512])).hexdigest()
     d = _run_verify(verify_driver, str(p), [(1, new1), (1, new1), (0, hexes[0])], index=True)
     assert d.returncode == 0, d.stderr
+
+
+@pytest.mark.parametrize("settle_ms", ["0", "2000"])
+def test_verify_chunk_hash_index_not_stale(pkg, dev, oracle, verify_driver, tmp_path, settle_ms):
+    """The sender re-verifies every GET against the master file (chunk.c:
+    204-217).  After the index is built (2nd verify), the file is rewritten in
+    place, same size, with its old mtime put back: the stale hash of the
+    changed chunk must now fail with exit(-1) (the index is keyed on ctime
+    too, and a file changed less than the settle time ago is re-hashed per
+    call), and the new hash must pass."""
+    import hashlib
+    data = oracle.synth_chunks(700, 3, L512).tobytes()
+    p = tmp_path / "master.dat"
+    p.write_bytes(data)
+    os.utime(p, ns=(10**18, 10**18))
+    data2 = bytearray(data)
+    data2[L512 + 77] ^= 0x01
+    q = tmp_path / "new.dat"
+    q.write_bytes(bytes(data2))
+    old = [hashlib.sha1(data[i * L512:(i + 1) * L512]).hexdigest() for i in range(3)]
+    new1 = hashlib.sha1(bytes(data2[L512:2 * L512])).hexdigest()
+    seq = [(0, old[0]), (1, old[1]), (2, old[2]), (1, old[1]), ("W", str(q))]
+    r = _run_verify(verify_driver, str(p), seq + [(1, old[1])], settle_ms=settle_ms)
+    assert r.returncode == 255, (r.stdout, r.stderr)
+    assert "Unmatched chunk hashes" in r.stderr and new1 in r.stderr
+    assert r.stdout.count("ok ") == 4 and "rewrote" in r.stdout
+    assert os.stat(p).st_mtime_ns == 10**18
+    p.write_bytes(data)
+    os.utime(p, ns=(10**18, 10**18))
+    r = _run_verify(verify_driver, str(p), seq + [(1, new1), (0, old[0]), (1, new1)], settle_ms=settle_ms)
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.count("ok ") == 7
 
 
 _MAKE_CHUNKS_DRIVER = r'''
