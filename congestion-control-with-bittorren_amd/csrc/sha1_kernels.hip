@@ -44,6 +44,8 @@
 #include <stdint.h>
 
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 
 #include "sha1_device.hpp"
 #include "sha1_kernels.h"
@@ -1156,6 +1158,66 @@ __global__ __launch_bounds__(kMixedThreads) void sha1_mixed_kernel(BatchArgs A) 
     fused_coop_body<0>(A, g * 64u + (threadIdx.x & 63u), lds + wave * kCoopWaveBytes);
 }
 
+// Persistent-dispatch variant of the mixed kernel (BASELINE config 5 names
+// "persistent-kernel dispatch"): one 512-thread
+// workgroup per CU (all 160 KiB of LDS each, so one resident per CU) pulls
+// the plan's jobs in order from a device counter (plan[3], zeroed by the
+// planner on the same stream) until the list is empty.  The job list is the
+// plan's: jobs 0 .. H-1 one split group each, then fused jobs of F groups (or
+// mode 1: pairs in the 8-wave split shape).  Against the hardware dispatch
+// of sha1_mixed_kernel (workgroup i goes to XCD i % 8 and waits for a CU of
+// that XCD) any CU that frees takes the next job: one global greedy queue
+// instead of eight.  Every wave stays in the loop, so the waves a split job
+// does not use pass the same number of workgroup barriers as the job's
+// waves (idle_barriers): units + 1 for a split job, plus the two of the
+// 8-wave shape's length exchange.
+__device__ __forceinline__ uint32_t group_units(const BatchArgs& A, uint32_t group, uint32_t U) {
+    const uint32_t e = group * 64u + (threadIdx.x & 63u);
+    const bool valid = e < A.n;
+    Entry en = fetch_entry(A, valid ? e : min(group * 64u, A.n - 1u));
+    const uint32_t T = valid ? total_blocks(en.len) : 0u;
+    const uint32_t Tmax = __builtin_amdgcn_readfirstlane(wave_max(T));
+    return (Tmax + 2u * U - 1u) / (2u * U) * 2u;
+}
+
+__device__ __forceinline__ void idle_barriers(uint32_t n) {
+    for (uint32_t i = 0; i < n; ++i) split_barrier();
+}
+
+__global__ __launch_bounds__(kMixedThreads) void sha1_mixed_persistent_kernel(BatchArgs A, uint32_t* queue) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[160 * 1024];
+    const uint32_t mode = A.plan[0], H = A.plan[1], F = A.plan[2];
+    const uint32_t groups = (A.n + 63u) / 64u;
+    const uint32_t jobs = mode == 1 ? (groups + 1u) / 2u : H + (groups - H + F - 1u) / F;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    uint32_t* slot = reinterpret_cast<uint32_t*>(lds);  // free between jobs
+    for (;;) {
+        if (threadIdx.x == 0) slot[0] = atomicAdd(queue, 1u);
+        __syncthreads();
+        const uint32_t job = __builtin_amdgcn_readfirstlane(slot[0]);
+        __syncthreads();  // every wave has the job before the LDS is reused
+        if (job >= jobs) break;
+        if (mode == 1) {
+            if (wave == 4 || wave == 6) {  // the 8-wave shape's empty waves
+                const uint32_t u = max(group_units(A, 2u * job, 2), 2u * job + 1u < groups
+                                                                        ? group_units(A, 2u * job + 1u, 2)
+                                                                        : 0u);
+                idle_barriers(2u + u + 1u);
+            } else {
+                split_body<2, 2, kSplit8V, 2>(A, lds, job);
+            }
+        } else if (job < H) {
+            if (wave == 0 || wave == 1 || wave == 3)  // the one-group shape (wave 2 empty)
+                split_body<4, 1, kSplitV<4>, kSplitNProd<4>>(A, lds, job);
+            else
+                idle_barriers(group_units(A, job, 4) + 1u);
+        } else {
+            const uint32_t g = H + (job - H) * F + wave;
+            if (wave < F && g < groups) fused_coop_body<0>(A, g * 64u + (threadIdx.x & 63u), lds + wave * kCoopWaveBytes);
+        }
+    }
+}
+
 // Makespan model of a sorted ragged batch, microseconds per 64-byte block of
 // a group of 64 chunks, measured on MI355X:
 //   chain: time of one group's block when it runs in that shape
@@ -1282,6 +1344,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
                                                                   uint32_t* plan) {
     const uint32_t n = A.n;
     const uint32_t t = threadIdx.x;
+    if (t == 0) plan[3] = 0u;  // the persistent kernel's job counter
     if (forced) {
         if (t == 0) {
             plan[0] = fmode;
@@ -1641,7 +1704,16 @@ hipError_t launch_mixed(const BatchArgs& A, const uint32_t* sorted_len, uint32_t
     if (e != hipSuccess) return e;
     BatchArgs B = A;
     B.plan = plan;
-    hipLaunchKernelGGL(sha1_mixed_kernel, dim3(grid), dim3(kMixedThreads), 0, st, B);
+    // SHA1CHUNK_MIXED_DISPATCH=persistent: the work-queue variant (one
+    // workgroup per CU pulling the plan's jobs), A/B against the hardware
+    // dispatch
+    const char* disp = getenv("SHA1CHUNK_MIXED_DISPATCH");
+    const bool persistent = disp && !strcmp(disp, "persistent");
+    if (persistent)
+        hipLaunchKernelGGL(sha1_mixed_persistent_kernel, dim3((uint32_t)cus), dim3(kMixedThreads), 0, st, B,
+                           plan + 3);
+    else
+        hipLaunchKernelGGL(sha1_mixed_kernel, dim3(grid), dim3(kMixedThreads), 0, st, B);
     return hipGetLastError();
 }
 

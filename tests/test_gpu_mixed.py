@@ -170,6 +170,18 @@ def ragged(rng, n, long_n, long_lo, long_hi, short_hi, aligned=True):
     return host, off, lens
 
 
+@pytest.fixture(params=["hw", "persistent"])
+def dispatch(request, monkeypatch):
+    """The mixed kernel's two dispatches: hardware (one workgroup per job)
+    and persistent (one workgroup per CU pulling jobs from a device counter,
+    SHA1CHUNK_MIXED_DISPATCH=persistent)."""
+    if request.param == "persistent":
+        monkeypatch.setenv("SHA1CHUNK_MIXED_DISPATCH", "persistent")
+    else:
+        monkeypatch.delenv("SHA1CHUNK_MIXED_DISPATCH", raising=False)
+    return request.param
+
+
 def run(pkg, torch, host, off, lens, env, monkeypatch, kernel="auto"):
     for k in ("SHA1CHUNK_MIXED_PLAN", "SHA1CHUNK_MIXED_DEBUG", "SHA1CHUNK_MIXED"):
         monkeypatch.delenv(k, raising=False)
@@ -189,7 +201,7 @@ def _check(got, want, what):
 
 
 @pytest.mark.parametrize("aligned", [True, False])
-def test_mixed_every_plan_shape(pkg, dev, oracle, cus, monkeypatch, aligned):
+def test_mixed_every_plan_shape(pkg, dev, oracle, cus, monkeypatch, dispatch, aligned):
     """~1.2 x CUs groups: split head sizes 0, 1, odd, all; fused tails of 4
     and 8 groups per workgroup (last one partial); the 8-wave mode; the
     planner's own choice.  Misaligned starts take every kernel's per-lane
@@ -207,7 +219,7 @@ def test_mixed_every_plan_shape(pkg, dev, oracle, cus, monkeypatch, aligned):
         _check(got, want, f"plan {p or 'device'} aligned={aligned}")
 
 
-def test_mixed_head_capped_below_groups(pkg, dev, oracle, cus, monkeypatch):
+def test_mixed_head_capped_below_groups(pkg, dev, oracle, cus, monkeypatch, dispatch):
     """More than 4 x CUs groups: the model's split heads stop at hcap <
     groups, the all-split plan (H = G) is still allowed, and every plan's
     workgroups must cover every group."""
@@ -288,7 +300,7 @@ def test_mixed_planner_matches_model(pkg, dev, cus, monkeypatch, capfd, shape):
         assert d[i].tobytes() == hashlib.sha1(bytes(int(L))).digest()
 
 
-def test_mixed_beyond_simulated_group_count(pkg, dev, oracle, cus, monkeypatch, capfd):
+def test_mixed_beyond_simulated_group_count(pkg, dev, oracle, cus, monkeypatch, capfd, dispatch):
     """More groups than the planner keeps in LDS (SIM_MAX_G = 16384): the
     bounds-only plan, a grid of G workgroups, every digest against the
     oracle.  1.05 M short chunks (0 .. 300 bytes, a few of 40 KiB)."""
@@ -310,7 +322,7 @@ def test_mixed_beyond_simulated_group_count(pkg, dev, oracle, cus, monkeypatch, 
     assert model_makespan(B, cus, mode, H, F, P) <= best * (1 + 1e-9), ((mode, H, F), (bmode, bH, bF))
 
 
-def test_mixed_config5_law_at_4x(pkg, dev, oracle, cus, monkeypatch):
+def test_mixed_config5_law_at_4x(pkg, dev, oracle, cus, monkeypatch, dispatch):
     """BASELINE config 5's length law (4 KiB .. 1 MiB, ragged tails) at 65536
     chunks (12 GiB resident, 4 groups per CU): AUTO's mixed kernel against
     the plain fused kernel in caller order, the first 16384 digests against

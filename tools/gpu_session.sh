@@ -42,6 +42,10 @@ for s in $STEPS; do
                python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
            run pmc2 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
                python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ;;
+    mixedab) run mixedab_arrival 400 python tools/mixed_bench.py --chunks 16384,65536,131072,262144 --reps 3 \
+                 --modes auto,auto@persistent --layout arrival --out "$OUT/mixedab_arrival.json"
+             run mixedab_sorted 400 python tools/mixed_bench.py --chunks 65536,131072,262144 --reps 3 \
+                 --modes auto,auto@persistent --layout sorted --out "$OUT/mixedab_sorted.json" ;;
     *) echo "unknown step $s" ;;
     esac
 done

@@ -4,7 +4,8 @@ chunks): the same length law (4 KiB .. 1 MiB, every 7th length with a
 ragged tail; oracle_mixed_len restated with numpy) at N chunks, timed with
 several dispatches: auto (the mixed kernel's device plan above 256 groups),
 auto_nomixed (AUTO's uniform-batch rule: fused / 8-wave split), x_sorted
-(AUTO's longest-first sort, kernel x forced), x (kernel x in caller order).
+(AUTO's longest-first sort, kernel x forced), x (kernel x in caller order);
+any mode + "@persistent" runs the mixed kernel's work-queue dispatch.
 Digests of every mode must agree, and a sample is checked with hashlib.
 
   python tools/mixed_bench.py --chunks 16384,65536,131072 [--out FILE]
@@ -100,8 +101,10 @@ def main():
             # not.  "<x>_sorted" keeps AUTO's sort and forces kernel x behind
             # it (SHA1CHUNK_FORCE_KERNEL); split8 = the 8-wave two-pair layout
             # for every group, split4 = one group per CU with 4-block units.
+            mode_name = mode
+            mode, _, disp = mode.partition("@")  # <mode>@persistent: the work-queue dispatch
             base_mode, _, srt = mode.partition("_")
-            env = {}
+            env = {"SHA1CHUNK_MIXED_DISPATCH": disp} if disp else {}
             kernel = base_mode
             if base_mode.startswith("plan"):  # plan<mode>.<H>.<F>: the mixed kernel with a forced plan
                 kernel, env = "auto", {"SHA1CHUNK_MIXED_PLAN": base_mode[4:].replace(".", ",")}
@@ -145,7 +148,7 @@ def main():
             else:
                 ok = bool(np.array_equal(got, ref))
             sec = float(np.median(ts))
-            row = {"chunks": n, "mode": mode, "layout": a.layout + ("+misalign" if a.misalign else ""),
+            row = {"chunks": n, "mode": mode_name, "layout": a.layout + ("+misalign" if a.misalign else ""),
                    "uniform": a.uniform, "payload_bytes": nbytes, "ms": round(sec * 1e3, 3),
                    "payload_GiBps": round(nbytes / sec / 2**30, 2), "runs_ms": [round(t * 1e3, 3) for t in ts],
                    "longest_blocks": int(lens.max()) // 64 + 2, "parity": ok}
