@@ -317,10 +317,14 @@ int launch_checked(int kernel, const BatchArgs& A, hipStream_t st, int cus = 256
 // Mixed kernel for sorted ragged batches of more groups than CUs, unless an
 // A/B hook forces a kernel behind AUTO (SHA1CHUNK_FORCE_KERNEL) or
 // SHA1CHUNK_MIXED=0 turns it off (then AUTO's uniform-batch rule applies).
-bool use_mixed() {
+// SHA1CHUNK_MIXED=all also sends batches of <= CUs groups (every group its
+// own CU at launch) through it (A/B).
+bool use_mixed(size_t n, int cus) {
     if (getenv("SHA1CHUNK_FORCE_KERNEL")) return false;
     const char* e = getenv("SHA1CHUNK_MIXED");
-    return !(e && !strcmp(e, "0"));
+    if (e && !strcmp(e, "0")) return false;
+    if (e && !strcmp(e, "all")) return true;
+    return (n + 63) / 64 > size_t(cus);
 }
 
 // SHA1CHUNK_MIXED_PLAN="mode,H,F" replaces the device-side plan (tests and
@@ -646,7 +650,7 @@ int sha1chunk_hash_device_async(const void* d_base, const uint64_t* d_offsets,
         uint32_t* plan = nullptr;
         hipError_t e = sort_by_length_desc(d_lengths, A.n, &A.order, &sorted_len, &plan, &scratch, st);
         if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "length sort: %s", hipGetErrorString(e));
-        if ((n + 63) / 64 > size_t(D->cus) && use_mixed()) {
+        if (use_mixed(n, D->cus)) {
             rc = launch_mixed_checked(A, sorted_len, plan, D->cus, st);
             (void)hipFreeAsync(scratch, st);
             return rc;

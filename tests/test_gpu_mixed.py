@@ -172,13 +172,10 @@ def ragged(rng, n, long_n, long_lo, long_hi, short_hi, aligned=True):
 
 @pytest.fixture(params=["hw", "persistent"])
 def dispatch(request, monkeypatch):
-    """The mixed kernel's two dispatches: hardware (one workgroup per job)
-    and persistent (one workgroup per CU pulling jobs from a device counter,
-    SHA1CHUNK_MIXED_DISPATCH=persistent)."""
-    if request.param == "persistent":
-        monkeypatch.setenv("SHA1CHUNK_MIXED_DISPATCH", "persistent")
-    else:
-        monkeypatch.delenv("SHA1CHUNK_MIXED_DISPATCH", raising=False)
+    """The mixed kernel's two dispatches: persistent (the default: one
+    workgroup per CU pulling jobs from a device counter) and hardware (one
+    workgroup per job, SHA1CHUNK_MIXED_DISPATCH=hw)."""
+    monkeypatch.setenv("SHA1CHUNK_MIXED_DISPATCH", request.param)
     return request.param
 
 

@@ -46,6 +46,18 @@ for s in $STEPS; do
                  --modes auto,auto@persistent --layout arrival --out "$OUT/mixedab_arrival.json"
              run mixedab_sorted 400 python tools/mixed_bench.py --chunks 65536,131072,262144 --reps 3 \
                  --modes auto,auto@persistent --layout sorted --out "$OUT/mixedab_sorted.json" ;;
+    mixedsweep)
+        P=""
+        for h in 0 32 64 96 107 128 160 192 256 384 512; do for f in 4 8; do P="$P,plan0.$h.$f,plan0.$h.$f@persistent"; done; done
+        P="auto,auto@persistent,plan1.0.0,plan1.0.0@persistent$P"
+        for lay in arrival sorted; do
+            run mixedsweep_$lay 500 python tools/mixed_bench.py --chunks 131072,262144 --reps 3 \
+                --modes "$P" --layout $lay --out "$OUT/mixedsweep_$lay.json"
+        done ;;
+    pmcshape) for n in 4096 32768 131072; do run pmc_$n 700 bash tools/pmc_shape.sh "$OUT/pmc_$n" $n; done ;;
+    shard) run shard32768 300 python bench.py --chunks 32768 --steps 20 --warmup 2 --no-cpu-baseline --no-latency --strong-total 0
+           run cfg5 300 python tools/mixed_bench.py --chunks 16384 --reps 5 --modes auto,auto_mixedall,auto_mixedall@hw \
+               --layout arrival --out "$OUT/cfg5.json" ;;
     *) echo "unknown step $s" ;;
     esac
 done

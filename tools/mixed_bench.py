@@ -5,7 +5,8 @@ ragged tail; oracle_mixed_len restated with numpy) at N chunks, timed with
 several dispatches: auto (the mixed kernel's device plan above 256 groups),
 auto_nomixed (AUTO's uniform-batch rule: fused / 8-wave split), x_sorted
 (AUTO's longest-first sort, kernel x forced), x (kernel x in caller order);
-any mode + "@persistent" runs the mixed kernel's work-queue dispatch.
+any mode + "@hw" / "@persistent" selects the mixed kernel's dispatch (one
+workgroup per job / the default work queue, one workgroup per CU).
 Digests of every mode must agree, and a sample is checked with hashlib.
 
   python tools/mixed_bench.py --chunks 16384,65536,131072 [--out FILE]
@@ -102,7 +103,7 @@ def main():
             # it (SHA1CHUNK_FORCE_KERNEL); split8 = the 8-wave two-pair layout
             # for every group, split4 = one group per CU with 4-block units.
             mode_name = mode
-            mode, _, disp = mode.partition("@")  # <mode>@persistent: the work-queue dispatch
+            mode, _, disp = mode.partition("@")  # <mode>@hw / @persistent: the mixed kernel's dispatch
             base_mode, _, srt = mode.partition("_")
             env = {"SHA1CHUNK_MIXED_DISPATCH": disp} if disp else {}
             kernel = base_mode
@@ -115,6 +116,8 @@ def main():
                 kernel = "auto"
             elif srt == "nomixed":  # AUTO without the mixed kernel (the uniform-batch rule)
                 env["SHA1CHUNK_MIXED"] = "0"
+            elif srt == "mixedall":  # the mixed kernel even at <= CUs groups
+                env["SHA1CHUNK_MIXED"] = "all"
             old = {k: os.environ.get(k) for k in env}
             os.environ.update(env)
             try:
