@@ -1555,7 +1555,7 @@ bool split_unit_built(int u) {
 #ifdef SHA1CHUNK_AB_VARIANTS
     static const int built[] = {1,  2,  3,  4,  8,  9,  10, 11, 12, 20, 21, 22, 23, 24, 26, 27,
                                 30, 31, 32, 33, 34, 36, 37, 42, 44, 45, 46, 504, 505, 506, 507,
-                                569, 577, 578, 579, 580, 581, 13, 583, 584, 585, 86, 87, 590};
+                                569, 577, 578, 579, 580, 581, 13, 583, 584, 585, 86, 87, 590, 14, 15};
     for (int b : built)
         if (u == b) return true;
     return false;
@@ -1635,6 +1635,14 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     case 585:  // the product's case 4 with schedule reads in four bursts of 5
         hipLaunchKernelGGL((sha1_split_kernel<4, 1, (77 & ~kVRead10) | kVCoop, 2>), dim3(groups), dim3(256), 0,
                            st, A);
+        break;
+    case 14:  // case 11 with the consumers at s_setprio 3 (round-3 A/B: LDS issue contention)
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, kSplit8V | kVPrio, 2>), dim3((groups + 1) / 2), dim3(512), 0,
+                           st, A);
+        break;
+    case 15:  // case 13 with the consumers at s_setprio 3
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, (kSplit8V & ~kVCoop) | kVPrio, 2>), dim3((groups + 1) / 2),
+                           dim3(512), 0, st, A);
         break;
     case 13:  // case 11 with lane-per-chunk producer loads (round-2 A/B of kVCoop)
         hipLaunchKernelGGL((sha1_split_kernel<2, 2, kSplit8V & ~kVCoop, 2>), dim3((groups + 1) / 2), dim3(512), 0,

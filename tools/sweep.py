@@ -25,6 +25,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--out", default=None)
     ap.add_argument("--lib", default=None, help="A/B: load this libsha1chunk.so instead")
+    ap.add_argument("--burst", type=int, default=1,
+                    help="launches per kernel per round, back to back; the last ceil(burst/2) "
+                         "are timed (the chip's clock ramps over the first few ms of a full load)")
     ap.add_argument("--no-check", action="store_true",
                     help="timing only: skip the cross-kernel digest check (diagnostic variants)")
     a = ap.parse_args()
@@ -48,7 +51,6 @@ def main():
         for _ in range(a.rounds):
             for k in kernels:
                 dig = torch.zeros((n, 20), dtype=torch.uint8, device="cuda")
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 name = k
                 if k.startswith("split") and k[5:].isdigit():  # split<U>: force the unit size
                     os.environ["SHA1CHUNK_SPLIT_UNIT"] = k[5:]
@@ -56,13 +58,17 @@ def main():
                 if k.startswith("fused") and k[5:].isdigit():  # fused<RV>: round-sum form (A/B lib)
                     os.environ["SHA1CHUNK_FUSED_VARIANT"] = k[5:]
                     name = "fused"
-                e0.record()
-                pkg.hash_uniform_device(buf, L, n, dig, kernel=name)
-                e1.record()
+                evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                       for _ in range(max(1, a.burst))]
+                for e0, e1 in evs:
+                    e0.record()
+                    pkg.hash_uniform_device(buf, L, n, dig, kernel=name)
+                    e1.record()
                 torch.cuda.synchronize()
                 os.environ.pop("SHA1CHUNK_SPLIT_UNIT", None)
                 os.environ.pop("SHA1CHUNK_FUSED_VARIANT", None)
-                times[k].append(e0.elapsed_time(e1))
+                timed = evs[len(evs) // 2:]
+                times[k].append(float(np.mean([e0.elapsed_time(e1) for e0, e1 in timed])))
                 d = dig.cpu().numpy()
                 if ref is None:
                     ref = d
