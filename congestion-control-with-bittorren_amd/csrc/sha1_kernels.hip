@@ -1575,9 +1575,20 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
                            st, A);
         break;
     case 11:  // <= 2 groups per CU: 2 pairs x (consumer + 2 producers), 2-block
-              // units, 8-wave layout, producer SIMDs crossed between the pairs
-        hipLaunchKernelGGL((sha1_split_kernel<2, 2, kSplit8V, 2>), dim3((groups + 1) / 2), dim3(512), 0,
-                           st, A);
+              // units, 8-wave layout, producer SIMDs crossed between the pairs.
+              // Chunks back to back (the uniform layout): lane-per-chunk producer
+              // loads -- no TLB thrash to avoid, and the shared loads' LDS
+              // transpose adds to this shape's LDS contention (LDS-issue stall
+              // 9.8 % of wave time against 1.9 % at one group per CU): 6.33
+              // against 6.41 ms at 32768 chunks, steady clock
+              // (profiles/shard_ab_r03.json).  Ragged (possibly scattered)
+              // chunks keep the shared loads.
+        if (A.off == nullptr && A.order == nullptr)
+            hipLaunchKernelGGL((sha1_split_kernel<2, 2, kSplit8V & ~kVCoop, 2>), dim3((groups + 1) / 2), dim3(512),
+                               0, st, A);
+        else
+            hipLaunchKernelGGL((sha1_split_kernel<2, 2, kSplit8V, 2>), dim3((groups + 1) / 2), dim3(512), 0,
+                               st, A);
         break;
 #ifdef SHA1CHUNK_AB_VARIANTS
     // The shapes and variants of the split-kernel study (profiles/sweep_r01.json,

@@ -59,7 +59,9 @@ for s in $STEPS; do
            run cfg5 300 python tools/mixed_bench.py --chunks 16384 --reps 5 --modes auto,auto_mixedall,auto_mixedall@hw \
                --layout arrival --out "$OUT/cfg5.json" ;;
     shardab) run shardab 600 python tools/sweep.py --lib congestion-control-with-bittorren_amd/build-ab/libsha1chunk.so \
-                 --chunks 32768 --kernels split11,split14,split13,split15 --rounds 5 --burst 8 --out "$OUT/shardab.json" ;;
+                 --chunks 32768 --kernels split11,split14,split13,split15 --rounds 5 --burst 8 --out "$OUT/shardab.json"
+             run shardprod 300 python tools/sweep.py --chunks 32768,4096 --kernels split --rounds 5 --burst 8 \
+                 --out "$OUT/shardprod.json" ;;
     *) echo "unknown step $s" ;;
     esac
 done
