@@ -36,8 +36,7 @@ for s in $STEPS; do
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     sweep) run sweep 600 python tools/sweep.py --chunks 1024,4096,16384,65536,131072 --rounds 2 --out "$OUT/sweep.json" ;;
     bench) run bench 600 python bench.py --steps 10 --warmup 2 ;;
-    prof)  run rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o run -- \
-               python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline ;;
+    prof)  run rocprof 900 bash tools/profile_bench.sh $TAG ;;
     pmc)   run pmc 600 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o run -- \
                python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline
            run pmc2 600 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o run -- \
