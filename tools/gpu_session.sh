@@ -61,6 +61,8 @@ for s in $STEPS; do
                  --chunks 32768 --kernels split11,split14,split13,split15 --rounds 5 --burst 8 --out "$OUT/shardab.json"
              run shardprod 300 python tools/sweep.py --chunks 32768,4096 --kernels split --rounds 5 --burst 8 \
                  --out "$OUT/shardprod.json" ;;
+    rehearse2) SHA1_BENCH_DIST_BACKEND=gloo run rehearse2 600 python -m torch.distributed.run --nnodes=1 \
+                   --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 2 ;;
     *) echo "unknown step $s" ;;
     esac
 done
