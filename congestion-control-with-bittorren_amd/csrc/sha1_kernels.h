@@ -42,6 +42,29 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st);
 uint32_t mixed_grid(uint32_t groups, int cus, uint32_t* hcap);
 hipError_t launch_mixed(const BatchArgs& A, const uint32_t* sorted_len, uint32_t* plan, int cus,
                         const int* forced, hipStream_t st);
+// Persistent verify-queue drain (sha1_kernels.hip, vq drain; host side in
+// sha1_runtime.hip, the persistent sha1chunk_vq).  The queue's rings live in
+// coherent pinned host memory, which the kernel reads over PCIe (no copy
+// engine, no launch per batch); results go back to host memory.
+struct VqDrainArgs {
+    const uint8_t* data;     // host: chunk bytes (ring)
+    const uint64_t* off;     // host: per slot, byte offset into data
+    const uint32_t* len;     // host: per slot, chunk length
+    const uint8_t* exp;      // host: per slot, expected digest (20 B)
+    const uint32_t* grp;     // host: per group ring entry {first slot, count}
+    const uint32_t* pub;     // host: groups published so far
+    const uint32_t* stop;    // host: nonzero = exit once nothing is claimable
+    uint32_t* alive;         // host: per workgroup, 1 while it may still claim
+    uint8_t* res;            // host: per slot, 0 match / 1 mismatch
+    uint32_t* done;          // host: per group ring entry, group index + 1 when done
+    uint8_t* dig;            // device: per slot, digest scratch
+    uint32_t* claim;         // device: groups claimed so far
+    uint32_t grp_ring;       // group ring entries
+    uint32_t pad;
+    uint64_t idle_ticks;     // 100 MHz ticks without work before a workgroup exits
+};
+hipError_t launch_vq_drain(const VqDrainArgs& Q, uint32_t grid, hipStream_t st);
+
 hipError_t launch_synth(uint8_t* dst, const uint64_t* off, const uint32_t* lens, uint32_t ulen,
                         uint64_t first, uint64_t count, uint64_t seed, hipStream_t st);
 hipError_t launch_compare(const uint8_t* dig, const uint8_t* exp, uint32_t n, uint8_t* mismatch,

@@ -1218,6 +1218,104 @@ __global__ __launch_bounds__(kMixedThreads) void sha1_mixed_persistent_kernel(Ba
     }
 }
 
+// ---------------------------------------------------- verify-queue drain ----
+// The persistent drain of the received-chunk verify queue (SURVEY 8f rank 2;
+// packet_handler.c:469-472 -> job.c:217-228 verify_hash).  One 512-thread
+// workgroup per CU loops: lane 0 claims the next published group of <= 64
+// chunks (a compare-and-swap on a device counter, below the host's `pub`),
+// the workgroup hashes it in the one-group split shape straight out of the
+// host ring (coherent pinned memory: every read goes over PCIe, nothing is
+// cached), wave 0 compares the 64 digests with the expected ones and
+// writes a 0/1 per chunk and the group's completion word to host memory.
+// Without work a workgroup sleeps (exponential backoff up to ~50 us) and
+// exits after `idle_ticks` of 100 MHz time, or at once when the host sets
+// `stop`.  Exit handshake (no lost group): the workgroup clears its alive
+// word, fences, and re-reads `pub`; the host stores `pub`, fences, and reads
+// the alive words.  At least one of them sees the other: either the
+// workgroup claims the new group or the host launches a new drain.
+constexpr uint32_t kVqIdle = 0xffffffffu, kVqExit = 0xfffffffeu;
+
+__device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Lane 0 only: a claimed group index, kVqIdle or kVqExit.
+__device__ uint32_t vq_next(const VqDrainArgs& Q, uint64_t last_work) {
+    for (int round = 0; round < 2; ++round) {
+        uint32_t p = ld_sys(Q.pub);
+        uint32_t c = __hip_atomic_load(Q.claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        while (c < p) {
+            if (__hip_atomic_compare_exchange_strong(Q.claim, &c, c + 1u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT))
+                return c;
+        }
+        if (ld_sys(Q.stop)) return kVqExit;
+        if (round == 1 || __builtin_amdgcn_s_memrealtime() - last_work <= Q.idle_ticks) return kVqIdle;
+        // idle too long: leave, unless a group was published meanwhile
+        st_sys(Q.alive + blockIdx.x, 0u);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+        if (__hip_atomic_load(Q.claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ld_sys(Q.pub)) return kVqExit;
+        st_sys(Q.alive + blockIdx.x, 1u);
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
+    }
+    return kVqIdle;
+}
+
+__global__ __launch_bounds__(kMixedThreads) void sha1_vq_drain_kernel(VqDrainArgs Q) {
+    __shared__ __attribute__((aligned(16))) uint8_t lds[160 * 1024];
+    uint32_t* slot = reinterpret_cast<uint32_t*>(lds);  // free between jobs
+    const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    uint64_t last_work = __builtin_amdgcn_s_memrealtime();
+    uint32_t backoff = 1;
+    for (;;) {
+        if (threadIdx.x == 0) slot[0] = vq_next(Q, last_work);
+        __syncthreads();
+        const uint32_t g = __builtin_amdgcn_readfirstlane(slot[0]);
+        __syncthreads();  // every wave has the command before the LDS is reused
+        if (g == kVqExit) break;
+        if (g == kVqIdle) {
+            for (uint32_t i = 0; i < backoff; ++i) __builtin_amdgcn_s_sleep(127);  // ~3.4 us each
+            backoff = min(backoff * 2u, 16u);
+            continue;
+        }
+        backoff = 1;
+        const uint32_t gi = g % Q.grp_ring;
+        const uint32_t first = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(Q.grp + 2 * gi, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        const uint32_t count = __builtin_amdgcn_readfirstlane(
+            __hip_atomic_load(Q.grp + 2 * gi + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        BatchArgs A{};
+        A.base = Q.data;
+        A.off = Q.off + first;
+        A.len = Q.len + first;
+        A.n = count;
+        A.dig = Q.dig + 20ull * first;
+        if (wave == 0 || wave == 1 || wave == 3)  // the one-group split shape (wave 2 empty)
+            split_body<4, 1, kSplitV<4>, kSplitNProd<4>>(A, lds, 0);
+        else
+            idle_barriers(group_units(A, 0, 4) + 1u);
+        __syncthreads();
+        if (wave == 0) {  // the consumer wave re-reads the digests it wrote
+            uint32_t diff = 0;
+            if (lane < count) {
+                const uint32_t* d = reinterpret_cast<const uint32_t*>(A.dig + 20u * lane);
+                const uint32_t* x = reinterpret_cast<const uint32_t*>(Q.exp + 20ull * (first + lane));
+#pragma unroll
+                for (int i = 0; i < 5; ++i)
+                    diff |= d[i] ^ __hip_atomic_load(x + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                Q.res[first + lane] = diff ? 1 : 0;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+            if (lane == 0) st_sys(Q.done + gi, g + 1u);
+        }
+        last_work = __builtin_amdgcn_s_memrealtime();
+    }
+}
+
 // Makespan model of a sorted ragged batch, microseconds per 64-byte block of
 // a group of 64 chunks, measured on MI355X:
 //   chain: time of one group's block when it runs in that shape
@@ -1735,6 +1833,11 @@ hipError_t launch_mixed(const BatchArgs& A, const uint32_t* sorted_len, uint32_t
                            plan + 3);
     else
         hipLaunchKernelGGL(sha1_mixed_kernel, dim3(grid), dim3(kMixedThreads), 0, st, B);
+    return hipGetLastError();
+}
+
+hipError_t launch_vq_drain(const VqDrainArgs& Q, uint32_t grid, hipStream_t st) {
+    hipLaunchKernelGGL(sha1_vq_drain_kernel, dim3(grid), dim3(kMixedThreads), 0, st, Q);
     return hipGetLastError();
 }
 

@@ -10,6 +10,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cerrno>
 #include <cstdarg>
@@ -1057,7 +1058,12 @@ struct VqSet {
 };
 }  // namespace
 
+namespace {
+struct Pvq;
+}
+
 struct sha1chunk_vq {
+    Pvq* pv = nullptr;  // the persistent drain (SHA1CHUNK_VQ_MODE=persistent), else batch launches
     int dev = 0;
     int cus = 256;
     size_t batch = 0;  // launch threshold
@@ -1153,6 +1159,292 @@ int vq_maybe_launch(sha1chunk_vq* q) {
     return SHA1CHUNK_OK;
 }
 
+// ------------------------------------------------ persistent verify queue --
+// sha1chunk_vq with a persistent drain kernel (sha1_vq_drain_kernel): the
+// host copies each submitted chunk into a ring in pinned, uncached host
+// memory, writes its length and expected digest next to it, and publishes
+// groups of up to 64 chunks by bumping `pub`.  The drain -- one workgroup
+// per CU, started when work is published and no workgroup is alive, gone
+// again after SHA1CHUNK_VQ_IDLE_MS (default 20) without work -- reads the
+// ring over PCIe, hashes each group in the one-group split shape and writes
+// one 0/1 per chunk plus the group's completion word back to host memory.
+// No copy engine, no launch per batch: a chunk starts hashing as soon as
+// its group is published.  A group is published when it holds
+// min(batch, 64) chunks, or at once while fewer groups are in flight than
+// the device has CUs (so at low rates every chunk goes alone and comes back
+// after its own serial chain, ~6 ms for 512 KiB, whatever the batch size).
+// Positions in both rings are monotonic counters (physical = counter mod
+// ring size); a group never wraps either ring.
+constexpr uint32_t kPvqMaxGroup = 64;
+struct PvqCtl {
+    uint32_t pub;   // groups published (host store, release)
+    uint32_t stop;  // destroy: exit once nothing is claimable
+    uint32_t pad[30];
+    uint32_t alive[1024];
+};
+struct PvqGroup {
+    uint64_t g;         // group index
+    uint64_t slot0;     // first slot (monotonic)
+    uint32_t count;
+    uint64_t byte_end;  // byte ring position after its last chunk (monotonic)
+    bool collected;
+};
+struct Pvq {
+    int dev = 0, cus = 256;
+    uint32_t nslots = 0;  // slot ring (chunks) = group ring entries
+    uint64_t nbytes = 0;  // data ring bytes
+    uint32_t maxlen = 0;
+    uint32_t group_max = kPvqMaxGroup;
+    uint64_t idle_ticks = 0;
+    // pinned, uncached host memory: data ring, then the per-slot and
+    // per-group arrays, then the control words
+    uint8_t* hmem = nullptr;
+    uint8_t* data = nullptr;
+    uint64_t* off = nullptr;
+    uint32_t* grp = nullptr;
+    uint32_t* len = nullptr;
+    uint32_t* done = nullptr;
+    uint8_t* exp = nullptr;
+    uint8_t* res = nullptr;
+    PvqCtl* ctl = nullptr;
+    // device memory: digest scratch + the claim counter
+    uint8_t* dmem = nullptr;
+    std::vector<uint64_t> tags;
+    uint64_t slot_head = 0, slot_tail = 0, byte_head = 0, byte_tail = 0;
+    uint64_t open_slot0 = 0;
+    uint32_t open_count = 0;
+    uint64_t next_g = 0;
+    std::deque<PvqGroup> groups;  // published, oldest first
+    size_t inflight = 0;          // published, not yet collected
+    std::deque<std::pair<uint64_t, uint8_t>> ready;
+    size_t pending = 0;
+    hipStream_t stream[2] = {nullptr, nullptr};
+    int next_stream = 0;
+    PartPool* copier = nullptr;
+};
+
+uint64_t env_u64(const char* name, uint64_t dflt) {
+    const char* e = getenv(name);
+    return e ? strtoull(e, nullptr, 10) : dflt;
+}
+
+int pvq_launch(Pvq* P) {
+    // every workgroup of the new drain counts as alive from here on, so a
+    // submit right after does not launch another one
+    for (int w = 0; w < P->cus; ++w) __atomic_store_n(&P->ctl->alive[w], 1u, __ATOMIC_RELEASE);
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    VqDrainArgs Q{};
+    Q.data = P->data;
+    Q.off = P->off;
+    Q.len = P->len;
+    Q.exp = P->exp;
+    Q.grp = P->grp;
+    Q.pub = &P->ctl->pub;
+    Q.stop = &P->ctl->stop;
+    Q.alive = P->ctl->alive;
+    Q.res = P->res;
+    Q.done = P->done;
+    Q.dig = P->dmem;
+    Q.claim = reinterpret_cast<uint32_t*>(P->dmem + 20ull * P->nslots);
+    Q.grp_ring = P->nslots;
+    Q.idle_ticks = P->idle_ticks;
+    const int k = P->next_stream;
+    P->next_stream ^= 1;  // a new drain may start while an old one is still leaving
+    HIP_TRY(hipSetDevice(P->dev));
+    hipError_t e = launch_vq_drain(Q, static_cast<uint32_t>(P->cus), P->stream[k]);
+    if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "vq drain launch: %s", hipGetErrorString(e));
+    return SHA1CHUNK_OK;
+}
+
+// After `pub` moved: launch a drain unless some workgroup is still alive
+// (it then sees the new groups: the exit handshake in sha1_kernels.hip).
+int pvq_ensure_drain(Pvq* P) {
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    for (int w = 0; w < P->cus; ++w)
+        if (__atomic_load_n(&P->ctl->alive[w], __ATOMIC_ACQUIRE)) return SHA1CHUNK_OK;
+    return pvq_launch(P);
+}
+
+int pvq_publish(Pvq* P) {
+    if (P->open_count == 0) return SHA1CHUNK_OK;
+    const uint64_t g = P->next_g++;
+    const uint32_t gi = static_cast<uint32_t>(g % P->nslots);
+    P->grp[2 * gi] = static_cast<uint32_t>(P->open_slot0 % P->nslots);
+    P->grp[2 * gi + 1] = P->open_count;
+    P->groups.push_back(PvqGroup{g, P->open_slot0, P->open_count, P->byte_tail, false});
+    ++P->inflight;
+    P->open_slot0 = P->slot_tail;
+    P->open_count = 0;
+    // the group's bytes, lengths, digests and descriptor are written: release them
+    __atomic_store_n(&P->ctl->pub, static_cast<uint32_t>(g + 1), __ATOMIC_RELEASE);
+    return pvq_ensure_drain(P);
+}
+
+// Collect every finished group (in any order) and free ring space up to
+// the oldest unfinished one.
+int pvq_reap(Pvq* P) {
+    for (auto& G : P->groups) {
+        if (G.collected) continue;
+        const uint32_t gi = static_cast<uint32_t>(G.g % P->nslots);
+        if (__atomic_load_n(&P->done[gi], __ATOMIC_ACQUIRE) != static_cast<uint32_t>(G.g + 1)) continue;
+        for (uint32_t j = 0; j < G.count; ++j) {
+            const uint64_t sl = (G.slot0 + j) % P->nslots;
+            P->ready.emplace_back(P->tags[sl], P->res[sl]);
+        }
+        G.collected = true;
+        --P->inflight;
+    }
+    while (!P->groups.empty() && P->groups.front().collected) {
+        P->slot_head = P->groups.front().slot0 + P->groups.front().count;
+        P->byte_head = P->groups.front().byte_end;
+        P->groups.pop_front();
+    }
+    if (P->groups.empty()) {
+        P->slot_head = P->open_slot0;
+        if (P->open_count == 0) P->byte_head = P->byte_tail;
+    }
+    return SHA1CHUNK_OK;
+}
+
+// Wait (bounded) until `pred` holds, reaping and keeping a drain alive.
+template <typename Pred>
+int pvq_wait(Pvq* P, Pred pred, const char* what) {
+    const auto t0 = std::chrono::steady_clock::now();
+    int rc;
+    for (;;) {
+        if ((rc = pvq_reap(P))) return rc;
+        if (pred()) return SHA1CHUNK_OK;
+        if (P->inflight && (rc = pvq_ensure_drain(P))) return rc;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
+            return fail(SHA1CHUNK_EHIP, "vq: %s timed out (drain not progressing)", what);
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
+void pvq_destroy(Pvq* P) {
+    if (!P) return;
+    (void)hipSetDevice(P->dev);
+    if (P->ctl) {
+        __atomic_store_n(&P->ctl->stop, 1u, __ATOMIC_RELEASE);
+        __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    }
+    for (int k = 0; k < 2; ++k) {
+        if (P->stream[k]) (void)hipStreamSynchronize(P->stream[k]);
+        if (P->stream[k]) (void)hipStreamDestroy(P->stream[k]);
+    }
+    if (P->dmem) (void)hipFree(P->dmem);
+    if (P->hmem) (void)hipHostFree(P->hmem);
+    delete P->copier;
+    delete P;
+}
+
+Pvq* pvq_create(Device* D, size_t batch, uint32_t max_chunk_len) {
+    auto* P = new Pvq();
+    P->dev = D->id;
+    P->cus = std::min(D->cus, 1024);
+    P->maxlen = max_chunk_len;
+    P->group_max = static_cast<uint32_t>(std::min<size_t>(batch, kPvqMaxGroup));
+    P->idle_ticks = env_u64("SHA1CHUNK_VQ_IDLE_MS", 20) * 100000ull;  // s_memrealtime: 100 MHz
+    const uint64_t stride = round_up(max_chunk_len, kAlign);
+    const uint64_t ring_mib = std::max<uint64_t>(env_u64("SHA1CHUNK_VQ_RING_MIB", 1024), 1);
+    P->nbytes = round_up(std::max<uint64_t>(ring_mib << 20, 2 * kPvqMaxGroup * stride), kAlign);
+    // slots: room for the ring's bytes in chunks of a quarter of the max length
+    P->nslots = static_cast<uint32_t>(std::min<uint64_t>(
+        std::max<uint64_t>(P->nbytes / std::max<uint64_t>(kAlign, stride / 4), 4 * kPvqMaxGroup), 1u << 20));
+    const size_t ns = P->nslots;
+    const size_t meta = round_up(ns * 45, 4096);  // off 8, grp 8, len 4, done 4, exp 20, res 1
+    const size_t hbytes = P->nbytes + meta + sizeof(PvqCtl);
+    if (hipHostMalloc(reinterpret_cast<void**>(&P->hmem), hbytes, hipHostMallocUncached) != hipSuccess) {
+        (void)hipGetLastError();
+        P->hmem = nullptr;
+        if (hipHostMalloc(reinterpret_cast<void**>(&P->hmem), hbytes, hipHostMallocCoherent) != hipSuccess) {
+            (void)hipGetLastError();
+            P->hmem = nullptr;
+            fail(SHA1CHUNK_ENOMEM, "vq: pinned ring of %zu bytes", hbytes);
+            pvq_destroy(P);
+            return nullptr;
+        }
+    }
+    memset(P->hmem + P->nbytes, 0, meta + sizeof(PvqCtl));
+    uint8_t* m = P->hmem + P->nbytes;
+    P->data = P->hmem;
+    P->off = reinterpret_cast<uint64_t*>(m);
+    P->grp = reinterpret_cast<uint32_t*>(m + ns * 8);
+    P->len = reinterpret_cast<uint32_t*>(m + ns * 16);
+    P->done = reinterpret_cast<uint32_t*>(m + ns * 20);
+    P->exp = m + ns * 24;
+    P->res = m + ns * 44;
+    P->ctl = reinterpret_cast<PvqCtl*>(P->hmem + P->nbytes + meta);
+    P->tags.assign(ns, 0);
+    if (hipMalloc(reinterpret_cast<void**>(&P->dmem), 20ull * ns + 256) != hipSuccess ||
+        hipMemset(P->dmem + 20ull * ns, 0, 256) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+        fail(SHA1CHUNK_ENOMEM, "vq: device scratch");
+        pvq_destroy(P);
+        return nullptr;
+    }
+    for (int k = 0; k < 2; ++k)
+        if (hipStreamCreateWithFlags(&P->stream[k], hipStreamNonBlocking) != hipSuccess) {
+            fail(SHA1CHUNK_EHIP, "vq: stream creation");
+            pvq_destroy(P);
+            return nullptr;
+        }
+    P->copier = new PartPool(vq_copy_helpers());
+    return P;
+}
+
+int pvq_submit(Pvq* P, const void* chunk, uint32_t len, const uint8_t expected[20], uint64_t tag) {
+    const uint64_t need = round_up(std::max<uint32_t>(len, 1), kAlign);
+    int rc;
+    // a group never wraps a ring: close it where either ring wraps
+    const bool slot_wrap = P->slot_tail != 0 && (P->slot_tail % P->nslots) == 0;
+    const bool byte_wrap = (P->byte_tail % P->nbytes) + need > P->nbytes;
+    if ((slot_wrap || byte_wrap) && (rc = pvq_publish(P))) return rc;
+    const uint64_t pos = byte_wrap ? P->byte_tail + (P->nbytes - P->byte_tail % P->nbytes) : P->byte_tail;
+    // room in both rings (a bounded wait for the drain to free some)
+    if ((rc = pvq_wait(P, [&] {
+             return P->slot_tail + 1 - P->slot_head <= P->nslots && pos + need - P->byte_head <= P->nbytes;
+         }, "submit (ring full)")))
+        return rc;
+    const uint64_t sl = P->slot_tail % P->nslots;
+    const uint64_t at = pos % P->nbytes;
+    if (len) pool_copy(*P->copier, P->data + at, static_cast<const uint8_t*>(chunk), len);
+    P->off[sl] = at;
+    P->len[sl] = len;
+    memcpy(P->exp + 20 * sl, expected, 20);
+    P->tags[sl] = tag;
+    if (P->open_count == 0) P->open_slot0 = P->slot_tail;
+    ++P->open_count;
+    ++P->slot_tail;
+    P->byte_tail = pos + need;
+    ++P->pending;
+    if ((rc = pvq_reap(P))) return rc;
+    if (P->open_count >= P->group_max || P->inflight < static_cast<size_t>(P->cus)) return pvq_publish(P);
+    return SHA1CHUNK_OK;
+}
+
+long pvq_poll(Pvq* P, uint64_t* tags, uint8_t* mismatch, size_t max, int wait) {
+    int rc;
+    if (wait) {
+        if ((rc = pvq_publish(P))) return rc;
+        if ((rc = pvq_wait(P, [&] { return P->inflight == 0; }, "poll(wait)"))) return rc;
+    } else {
+        if ((rc = pvq_reap(P))) return rc;
+        // an open group goes out once the device has room for it
+        if (P->open_count && P->inflight < static_cast<size_t>(P->cus) && (rc = pvq_publish(P))) return rc;
+        if (P->inflight && (rc = pvq_ensure_drain(P))) return rc;
+    }
+    size_t n = 0;
+    while (n < max && !P->ready.empty()) {
+        tags[n] = P->ready.front().first;
+        mismatch[n] = P->ready.front().second;
+        P->ready.pop_front();
+        ++n;
+    }
+    P->pending -= n;
+    return static_cast<long>(n);
+}
+
+
 size_t vq_cap(size_t batch) {
     const char* e = getenv("SHA1CHUNK_VQ_GROW");  // 0: launch at exactly `batch`
     if ((e && atoi(e) == 0) || batch >= 512) return batch;
@@ -1172,6 +1464,15 @@ sha1chunk_vq* sha1chunk_vq_create(size_t batch, uint32_t max_chunk_len) {
     if (get_device(&D)) return nullptr;
     auto* q = new sha1chunk_vq();
     q->dev = D->id;
+    const char* mode = getenv("SHA1CHUNK_VQ_MODE");
+    if (mode && !strcmp(mode, "persistent")) {
+        q->pv = pvq_create(D, batch, max_chunk_len);
+        if (!q->pv) {
+            delete q;
+            return nullptr;
+        }
+        return q;
+    }
     q->cus = D->cus;
     q->batch = batch;
     q->cap = vq_cap(batch);
@@ -1196,6 +1497,11 @@ sha1chunk_vq* sha1chunk_vq_create(size_t batch, uint32_t max_chunk_len) {
 int sha1chunk_vq_submit(sha1chunk_vq* q, const void* chunk, uint32_t len, const uint8_t expected[20],
                         uint64_t tag) {
     if (!q || (len && !chunk) || !expected) return fail(SHA1CHUNK_EINVAL, "vq: null argument");
+    if (q->pv) {
+        if (len > q->pv->maxlen)
+            return fail(SHA1CHUNK_EINVAL, "vq: chunk of %u bytes > max %u", len, q->pv->maxlen);
+        return pvq_submit(q->pv, chunk, len, expected, tag);
+    }
     if (len > q->maxlen) return fail(SHA1CHUNK_EINVAL, "vq: chunk of %u bytes > max %u", len, q->maxlen);
     VqSet* S = &q->set[q->fill];
     while (S->inflight) {  // the fill set is still on the device: drain in order
@@ -1224,6 +1530,7 @@ int sha1chunk_vq_submit(sha1chunk_vq* q, const void* chunk, uint32_t len, const 
 
 int sha1chunk_vq_flush(sha1chunk_vq* q) {
     if (!q) return fail(SHA1CHUNK_EINVAL, "vq: null queue");
+    if (q->pv) return pvq_publish(q->pv);
     if (q->set[q->fill].count == 0 || q->set[q->fill].inflight) return SHA1CHUNK_OK;
     int rc = vq_launch(q, q->fill);
     if (rc) return rc;
@@ -1233,6 +1540,7 @@ int sha1chunk_vq_flush(sha1chunk_vq* q) {
 
 long sha1chunk_vq_poll(sha1chunk_vq* q, uint64_t* tags, uint8_t* mismatch, size_t max, int wait) {
     if (!q || (max && (!tags || !mismatch))) return fail(SHA1CHUNK_EINVAL, "vq: null argument");
+    if (q->pv) return pvq_poll(q->pv, tags, mismatch, max, wait);
     int rc;
     if (wait) {
         if ((rc = sha1chunk_vq_flush(q))) return rc;
@@ -1253,10 +1561,15 @@ long sha1chunk_vq_poll(sha1chunk_vq* q, uint64_t* tags, uint8_t* mismatch, size_
     return static_cast<long>(n);
 }
 
-size_t sha1chunk_vq_pending(const sha1chunk_vq* q) { return q ? q->pending : 0; }
+size_t sha1chunk_vq_pending(const sha1chunk_vq* q) { return q ? (q->pv ? q->pv->pending : q->pending) : 0; }
 
 void sha1chunk_vq_destroy(sha1chunk_vq* q) {
     if (!q) return;
+    if (q->pv) {
+        pvq_destroy(q->pv);
+        delete q;
+        return;
+    }
     (void)hipSetDevice(q->dev);
     for (auto& S : q->set) {
         if (S.stream) (void)hipStreamSynchronize(S.stream);

@@ -124,10 +124,17 @@ def test_random_batches_mixed_kernel(pkg, dev, oracle, seed, monkeypatch):
 # off and 1 or 4 copy threads (chunks above 64 KiB are copied in pieces by the
 # copy pool).  Every tag must come back exactly once with verify_hash's 0/1,
 # and pending must count what is still owed.
+# Both queue implementations: batch launches and the persistent drain
+# (SHA1CHUNK_VQ_MODE=persistent, with a 1 ms idle exit and a small ring so
+# the drain leaves and is relaunched, and both rings wrap, within a test).
+@pytest.mark.parametrize("mode", ["batch", "persistent"])
 @pytest.mark.parametrize("seed", range(int(os.environ.get("SHA1CHUNK_FUZZ_SEEDS", "12")) // 2 + 1))
-def test_random_verify_queue_interleavings(pkg, dev, oracle, seed, monkeypatch):
+def test_random_verify_queue_interleavings(pkg, dev, oracle, seed, monkeypatch, mode):
     import time
     rng = np.random.default_rng(9900 + seed)
+    monkeypatch.setenv("SHA1CHUNK_VQ_MODE", mode)
+    monkeypatch.setenv("SHA1CHUNK_VQ_IDLE_MS", str(int(rng.choice([1, 20]))))
+    monkeypatch.setenv("SHA1CHUNK_VQ_RING_MIB", str(int(rng.choice([8, 64]))))
     monkeypatch.setenv("SHA1CHUNK_VQ_GROW", str(int(rng.integers(0, 2))))
     monkeypatch.setenv("SHA1CHUNK_VQ_THREADS", str(int(rng.choice([1, 4]))))
     batch = int(rng.choice([1, 3, 8, 32, 100]))

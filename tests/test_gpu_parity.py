@@ -499,7 +499,15 @@ def test_host_batch_all_devices_virtual(pkg, dev, tmp_path):
     assert r.returncode == 0 and "all-devices ok" in r.stdout, r.stdout + r.stderr
 
 
-def test_verify_queue_receive_path(pkg, dev, oracle, golden, fixture_files):
+@pytest.fixture(params=["batch", "persistent"])
+def vq_mode(request, monkeypatch):
+    """The verify queue's two implementations: batch launches, and the
+    persistent drain kernel reading a pinned host ring (SHA1CHUNK_VQ_MODE)."""
+    monkeypatch.setenv("SHA1CHUNK_VQ_MODE", request.param)
+    return request.param
+
+
+def test_verify_queue_receive_path(pkg, dev, oracle, golden, fixture_files, vq_mode):
     """Batched async verify (packet_handler.c:469-472 -> job.c:217): every
     result comes back exactly once with verify_hash's 0/1 convention."""
     rng = np.random.default_rng(77)
@@ -534,7 +542,7 @@ def test_verify_queue_receive_path(pkg, dev, oracle, golden, fixture_files):
 
 
 @pytest.mark.parametrize("grow", ["1", "0"])
-def test_verify_queue_full_batches_drain_by_polling(pkg, dev, monkeypatch, grow):
+def test_verify_queue_full_batches_drain_by_polling(pkg, dev, monkeypatch, grow, vq_mode):
     """Submissions in whole batches come back through non-blocking poll()
     alone (no flush, no wait): a batch held back to grow while two earlier
     ones are on the device is launched by a later poll once one finishes."""

@@ -1,0 +1,148 @@
+"""The persistent verify-queue drain (SHA1CHUNK_VQ_MODE=persistent): the
+received-chunk verify of packet_handler.c:469-472 -> job.c:217-228
+(verify_hash, 0 = match, 1 = mismatch) through sha1chunk_vq_*, with the
+chunks read by a persistent kernel straight from a pinned host ring.
+
+Checked here beyond the shared queue tests (test_gpu_parity.py,
+test_gpu_fuzz.py): a lone chunk comes back after its own serial chain with
+no flush and no batch to fill; the drain leaves when idle and is launched
+again by the next submit; both rings wrap many times with every result
+right; results come back for chunks of the reference's fixture file."""
+import hashlib
+import os
+import time
+
+import numpy as np
+import pytest
+
+L512 = 524288
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev(pkg):
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a device"
+    assert pkg.device_count() >= 1, pkg.lib().sha1chunk_last_error()
+    torch.cuda.set_device(0)
+    pkg.set_device(0)
+    return torch
+
+
+@pytest.fixture
+def persistent(monkeypatch):
+    monkeypatch.setenv("SHA1CHUNK_VQ_MODE", "persistent")
+
+
+def _poll_until(q, n, timeout=30.0):
+    got, t0 = {}, time.time()
+    while len(got) < n and time.time() - t0 < timeout:
+        for tag, m in q.poll():
+            assert tag not in got
+            got[tag] = m
+        time.sleep(0.0002)
+    return got, time.time() - t0
+
+
+def test_lone_chunk_needs_no_batch(pkg, dev, persistent, fixture_files, golden):
+    """One 512 KiB chunk in a queue of batch 256: its result comes back by
+    non-blocking polls alone, in about one chain time (~6 ms), not after 255
+    more chunks or a flush."""
+    chunk = fixture_files["tmp/C.tar"][:L512]
+    want = golden["fixtures"]["C.chunks_file"][0]
+    with pkg.VerifyQueue(batch=256, max_chunk_len=L512) as q:
+        # warm: the first drain launch loads the code object
+        q.submit(chunk, want, 1)
+        got, _ = _poll_until(q, 1)
+        assert got == {1: 0}
+        lat = []
+        for t in range(2, 7):
+            q.submit(chunk, want, t)
+            got, secs = _poll_until(q, 1)
+            assert got == {t: 0}
+            lat.append(secs)
+        print(f"lone-chunk verify latency (submit -> poll result): {[round(x * 1e3, 2) for x in lat]} ms")
+        assert min(lat) < 0.05, lat
+        assert q.pending == 0
+
+
+def test_drain_relaunched_after_idle_exit(pkg, dev, persistent, monkeypatch):
+    """With a 1 ms idle exit the drain leaves between bursts; each burst's
+    first submit launches it again, and every result of every burst comes
+    back (random 0/1, sparse tags)."""
+    monkeypatch.setenv("SHA1CHUNK_VQ_IDLE_MS", "1")
+    rng = np.random.default_rng(11)
+    want, got = {}, {}
+    with pkg.VerifyQueue(batch=16, max_chunk_len=65536) as q:
+        for burst in range(6):
+            for i in range(int(rng.integers(1, 40))):
+                b = rng.integers(0, 256, int(rng.integers(0, 65537)), dtype=np.uint8).tobytes()
+                d = hashlib.sha1(b).digest()
+                bad = bool(rng.random() < 0.3)
+                if bad:
+                    d = d[:5] + bytes([d[5] ^ 4]) + d[6:]
+                tag = burst * 1000 + i
+                want[tag] = int(bad)
+                q.submit(b, d, tag)
+            g, _ = _poll_until(q, sum(1 for t in want if t // 1000 == burst))
+            got.update(g)
+            time.sleep(0.02)  # > idle: the drain has exited
+        assert q.pending == 0
+    assert got == want
+
+
+def test_rings_wrap_many_times(pkg, dev, persistent, monkeypatch, oracle):
+    """A 4 MiB data ring and chunks up to 256 KiB: several thousand chunks
+    wrap the byte ring ~150 times and the slot ring many times; groups close
+    at every wrap; the submitter blocks while the ring is full.  Every
+    result is right (10 % corrupted expected digests)."""
+    monkeypatch.setenv("SHA1CHUNK_VQ_RING_MIB", "4")
+    rng = np.random.default_rng(4242)
+    n = 3000
+    lens = rng.integers(0, 262145, n)
+    lens[::17] = 262144
+    data = rng.integers(0, 256, 262144 + 8192, dtype=np.uint8)
+    want, got = {}, {}
+    with pkg.VerifyQueue(batch=64, max_chunk_len=262144) as q:
+        for t in range(n):
+            s = int(rng.integers(0, 8192))
+            chunk = data[s:s + int(lens[t])].tobytes()
+            d = oracle.shahash(chunk)
+            bad = t % 10 == 7
+            if bad:
+                d = bytes([d[0] ^ 1]) + d[1:]
+            want[t] = int(bad)
+            q.submit(chunk, d, t)
+            if t % 50 == 0:
+                for tag, m in q.poll():
+                    assert tag not in got
+                    got[tag] = m
+        for tag, m in q.poll(wait=True, max_results=1 << 16):
+            assert tag not in got
+            got[tag] = m
+        assert q.pending == 0
+    assert got == want
+
+
+def test_throughput_512k_chunks(pkg, dev, persistent):
+    """4096 x 512 KiB host chunks (2 GiB) through the persistent queue with
+    batch 64: every result right; the rate (PCIe-bound: the drain reads the
+    host ring over the link) is printed."""
+    rng = np.random.default_rng(3)
+    pool = [rng.integers(0, 256, L512, dtype=np.uint8).tobytes() for _ in range(8)]
+    digs = [hashlib.sha1(b).digest() for b in pool]
+    n = 4096
+    with pkg.VerifyQueue(batch=64, max_chunk_len=L512) as q:
+        t0 = time.perf_counter()
+        got = {}
+        for t in range(n):
+            d = digs[t % 8] if t % 13 else bytes(20)
+            q.submit(pool[t % 8], d, t)
+            if t % 64 == 63:
+                for tag, m in q.poll():
+                    got[tag] = m
+        for tag, m in q.poll(wait=True, max_results=1 << 16):
+            got[tag] = m
+        secs = time.perf_counter() - t0
+    print(f"persistent verify queue: {n} x 512 KiB in {secs * 1e3:.0f} ms = {n * L512 / secs / 2**30:.1f} GiB/s")
+    assert got == {t: (0 if t % 13 else 1) for t in range(n)}
