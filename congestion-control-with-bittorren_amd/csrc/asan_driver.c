@@ -96,7 +96,15 @@ int main(void) {
     CHECK(sha1chunk_verify_batch(buf, off, len, n, exp, mis, SHA1CHUNK_HOST) == 0, "verify_batch");
     for (size_t i = 0; i < n; ++i) CHECK(mis[i] == (i == 5 || i == 200), "verify_batch flag %zu", i);
 
-    /* verify queue: growth, polling, flush; every tag once with the right flag */
+    /* verify queue, both implementations (batch launches; the persistent
+     * drain reading a small pinned host ring, with a 1 ms idle exit so it
+     * leaves and is relaunched): growth, polling, flush; every tag once with
+     * the right flag */
+    static const char *modes[2] = {"batch", "persistent"};
+    for (int mo = 0; mo < 2; ++mo) {
+    setenv("SHA1CHUNK_VQ_MODE", modes[mo], 1);
+    setenv("SHA1CHUNK_VQ_IDLE_MS", "1", 1);
+    setenv("SHA1CHUNK_VQ_RING_MIB", "8", 1);
     sha1chunk_vq *q = sha1chunk_vq_create(16, L512);
     CHECK(q != NULL, "vq_create: %s", sha1chunk_last_error());
     size_t seen = 0;
@@ -125,6 +133,11 @@ int main(void) {
     }
     CHECK(seen == n && sha1chunk_vq_pending(q) == 0, "vq drained %zu of %zu", seen, n);
     sha1chunk_vq_destroy(q);
+    free(got);
+    }
+    unsetenv("SHA1CHUNK_VQ_MODE");
+    unsetenv("SHA1CHUNK_VQ_IDLE_MS");
+    unsetenv("SHA1CHUNK_VQ_RING_MIB");
 
     /* device ragged batch above one group per CU: the length sort, the
      * mixed kernel's planner and its forced plans (env parsing included),
@@ -199,7 +212,7 @@ int main(void) {
     free(hex);
     unlink(path);
 
-    free(off), free(len), free(buf), free(dig), free(mis), free(exp), free(got);
+    free(off), free(len), free(buf), free(dig), free(mis), free(exp);
     /* _exit: skip the HIP/HSA runtime's own teardown, which trips the ROCm
      * ASan runtime's device-allocator check after main (not this code) */
     if (fails) {
