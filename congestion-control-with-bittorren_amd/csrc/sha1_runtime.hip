@@ -1063,7 +1063,7 @@ struct Pvq;
 }
 
 struct sha1chunk_vq {
-    Pvq* pv = nullptr;  // the persistent drain (SHA1CHUNK_VQ_MODE=persistent), else batch launches
+    Pvq* pv = nullptr;  // the persistent drain (default), or null: batch launches (SHA1CHUNK_VQ_MODE=batch)
     int dev = 0;
     int cus = 256;
     size_t batch = 0;  // launch threshold
@@ -1464,8 +1464,9 @@ sha1chunk_vq* sha1chunk_vq_create(size_t batch, uint32_t max_chunk_len) {
     if (get_device(&D)) return nullptr;
     auto* q = new sha1chunk_vq();
     q->dev = D->id;
+    // the persistent drain unless SHA1CHUNK_VQ_MODE=batch (launch per batch)
     const char* mode = getenv("SHA1CHUNK_VQ_MODE");
-    if (mode && !strcmp(mode, "persistent")) {
+    if (!(mode && !strcmp(mode, "batch"))) {
         q->pv = pvq_create(D, batch, max_chunk_len);
         if (!q->pv) {
             delete q;

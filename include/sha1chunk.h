@@ -129,21 +129,34 @@ int sha1chunk_synth_fill_ragged_async(void *d_base, const uint64_t *d_offsets,
 /* ---- Asynchronous verify queue (the peer's receive path) --
  * The reference verifies each reassembled chunk synchronously inside its
  * select() loop (packet_handler.c:469-472 -> job.c:217 verify_hash).  A queue
- * batches them instead: submit() copies the chunk into pinned staging (the
- * caller may reuse its buffer at once) with its expected digest and a tag;
- * once `batch` submissions are pending (or on flush) the batch is hashed and
+ * verifies them asynchronously instead: submit() copies the chunk into pinned
+ * memory (the caller may reuse its buffer at once) with its expected digest
+ * and a tag, and poll() returns finished (tag, mismatch) pairs, mismatch
+ * following verify_hash: 0 = match, 1 = mismatch -> re-GET.
+ *
+ * Default: a persistent drain kernel.  The chunks go into a ring in pinned
+ * host memory (SHA1CHUNK_VQ_RING_MIB, default 1024) and are published in
+ * groups of up to min(batch, 64); while fewer groups are in flight than the
+ * GPU has CUs, each chunk goes out at once.  One workgroup per CU pulls the
+ * groups over PCIe, hashes and compares them, and writes the results back to
+ * host memory; it exits after SHA1CHUNK_VQ_IDLE_MS (default 20) without work
+ * and the next submit starts it again.  A lone chunk comes back after its
+ * own serial chain, with no batch to fill and no flush.
+ *
+ * SHA1CHUNK_VQ_MODE=batch: batches are launched as kernels.  Once `batch`
+ * submissions are pending (or on flush) the batch is hashed and
  * compared on the device asynchronously -- while two earlier batches are
  * still on the device a batch keeps growing by whole batches (up to 4 x
  * batch, at most 512; SHA1CHUNK_VQ_GROW=0 disables) and goes at the first
  * whole batch after one finishes (a submit or a poll notices); whole batches
- * therefore always come back through poll() without a flush; poll() returns
- * finished (tag, mismatch) pairs,
- * mismatch following verify_hash: 0 = match, 1 = mismatch -> re-GET.  One
- * queue per thread; queues on one device share nothing.  The copy is split
- * over SHA1CHUNK_VQ_THREADS threads (default 4, the caller included: three
- * helper threads per queue that spin briefly between submissions), and three
- * batch sets are in flight at once, so 1024-chunk batches run near the PCIe
- * rate. */
+ * therefore always come back through poll() without a flush.  Three batch
+ * sets are in flight at once.
+ *
+ * Both: one queue per thread; queues on one device share nothing.  The copy
+ * is split over SHA1CHUNK_VQ_THREADS threads (default 4, the caller
+ * included: three helper threads per queue that spin briefly between
+ * submissions).  Measured on 16384 x 512 KiB host chunks: 29-33 GiB/s
+ * persistent, 26-37 GiB/s batch. */
 typedef struct sha1chunk_vq sha1chunk_vq;
 /* NULL on failure (sha1chunk_last_error() says why). */
 sha1chunk_vq *sha1chunk_vq_create(size_t batch, uint32_t max_chunk_len);
