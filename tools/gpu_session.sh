@@ -65,6 +65,7 @@ for s in $STEPS; do
                    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 2 ;;
     vqbench) run vqbench 600 python tools/vq_bench.py --chunks 16384 --batches 64,256,1024 --reps 3 \
                  --out "$OUT/vq_bench.json" ;;
+    configs) run configs 900 python tools/bench_configs.py --out "$OUT/configs.json" ;;
     *) echo "unknown step $s" ;;
     esac
 done
