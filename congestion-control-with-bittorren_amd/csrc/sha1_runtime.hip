@@ -1280,13 +1280,20 @@ int pvq_publish(Pvq* P) {
     return pvq_ensure_drain(P);
 }
 
-// Collect every finished group (in any order) and free ring space up to
-// the oldest unfinished one.
+// Collect finished groups (in any order) and free ring space up to the
+// oldest unfinished one.  The drain claims groups in publication order and
+// runs at most one per CU at a time, so the scan stops after 2 x CUs
+// unfinished groups in a row: a submit costs O(CUs), not O(groups in flight).
 int pvq_reap(Pvq* P) {
+    size_t unfinished = 0;
     for (auto& G : P->groups) {
         if (G.collected) continue;
         const uint32_t gi = static_cast<uint32_t>(G.g % P->nslots);
-        if (__atomic_load_n(&P->done[gi], __ATOMIC_ACQUIRE) != static_cast<uint32_t>(G.g + 1)) continue;
+        if (__atomic_load_n(&P->done[gi], __ATOMIC_ACQUIRE) != static_cast<uint32_t>(G.g + 1)) {
+            if (++unfinished > 2 * static_cast<size_t>(P->cus)) break;
+            continue;
+        }
+        unfinished = 0;
         for (uint32_t j = 0; j < G.count; ++j) {
             const uint64_t sl = (G.slot0 + j) % P->nslots;
             P->ready.emplace_back(P->tags[sl], P->res[sl]);

@@ -146,3 +146,31 @@ def test_throughput_512k_chunks(pkg, dev, persistent):
         secs = time.perf_counter() - t0
     print(f"persistent verify queue: {n} x 512 KiB in {secs * 1e3:.0f} ms = {n * L512 / secs / 2**30:.1f} GiB/s")
     assert got == {t: (0 if t % 13 else 1) for t in range(n)}
+
+
+def test_small_chunks_many_groups(pkg, dev, persistent):
+    """20000 chunks of 0..8 KiB: thousands of small groups in flight at once
+    (the host's reap scan is bounded), every result right."""
+    rng = np.random.default_rng(8)
+    n = 20000
+    data = rng.integers(0, 256, 16384, dtype=np.uint8).tobytes()
+    lens = rng.integers(0, 8193, n)
+    want, got = {}, {}
+    with pkg.VerifyQueue(batch=64, max_chunk_len=8192) as q:
+        t0 = time.perf_counter()
+        for t in range(n):
+            s = int(t * 7 % 8192)
+            b = data[s:s + int(lens[t])]
+            d = hashlib.sha1(b).digest()
+            if t % 11 == 4:
+                d = d[:19] + bytes([d[19] ^ 0x10])
+            want[t] = int(t % 11 == 4)
+            q.submit(b, d, t)
+            if t % 256 == 255:
+                for tag, m in q.poll(max_results=1 << 16):
+                    got[tag] = m
+        for tag, m in q.poll(wait=True, max_results=1 << 16):
+            got[tag] = m
+        secs = time.perf_counter() - t0
+    print(f"persistent verify queue: {n} chunks of 0..8 KiB in {secs * 1e3:.0f} ms ({n / secs:.0f} chunks/s)")
+    assert got == want

@@ -24,6 +24,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--chunks", type=int, default=4096)
     ap.add_argument("--distinct", type=int, default=256, help="distinct host buffers reused round-robin")
+    ap.add_argument("--chunk-len", type=int, default=0, help="bytes per chunk (default CHUNK_LEN, 512 KiB)")
     ap.add_argument("--batches", default="64,256,1024")
     ap.add_argument("--reps", type=int, default=1, help="timed passes per batch size (best and median reported)")
     ap.add_argument("--modes", default="batch,persistent",
@@ -31,7 +32,7 @@ def main():
     ap.add_argument("--out", default="")
     a = ap.parse_args()
     pkg = importlib.import_module("congestion-control-with-bittorren_amd")
-    L = pkg.sha1chunk.CHUNK_LEN
+    L = a.chunk_len or pkg.sha1chunk.CHUNK_LEN
     rng = np.random.default_rng(5)
     bufs = [rng.integers(0, 256, L, dtype=np.uint8).tobytes() for _ in range(a.distinct)]
     digs = [hashlib.sha1(b).digest() for b in bufs]
