@@ -68,21 +68,24 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 #    streams: tools/issue_probe.hip -> profiles/issue_r01.json; the
 #    "vector-instruction ISSUE cost" row of MI355X_MICROARCH.md).  The floor
 #    is one chunk's serial chain: blocks x instructions x 4 cycles.
-#  * fused kernel (more groups): the SIMD's VALU time.  gfx950 SIMDs are 32
-#    lanes wide: a full-rate wave64 VALU op takes 2 cycles, the half-rate ones
-#    (v_alignbit, v_add3, v_perm, ...) 4 (tools/microbench.hip,
-#    profiles/microbench_ops_r01.json: ~1.1 vs ~1.9 ns).  Per block the fused
-#    loop has 400 half-rate + 221.75 full-rate VALU = 2043.5 SIMD cycles per
-#    wave of 64 chunks.
-# Measured counterpart of that model: the same compression on register data
-# with no memory traffic, every SIMD holding 8 waves, reaches 3940 GB/s of
-# message bytes (tools/microbench.hip compress_test "512 x 1024",
-# profiles/microbench_issue_r01.json): the chip lowers its clock under a
-# full VALU load, so this, not the 2.4 GHz model, is what a kernel can reach.
+#  * fused kernel (more groups): the SIMD's VALU time.  The fused loop issues
+#    621.75 VALU per block per wave of 64 chunks, and a SIMD completes about
+#    one VALU instruction every 4 cycles whatever its class: the PMC passes at
+#    131072 chunks (2 waves per SIMD) give 4.17 cycles per VALU per SIMD at the
+#    clock the chip holds, and 4 waves per SIMD take the same time per wave
+#    (profiles/pmc_shape_r03.json).  The round-2 model
+#    of 2 cycles for the "full-rate" ops (2043.5 cycles per block) is not
+#    reached by any kernel or microbenchmark here, so the ceiling below uses
+#    4 cycles per VALU: 2487 SIMD cycles per wave-block.
+# Measured counterpart: the same compression on register data with no
+# memory traffic, every SIMD holding 8 waves, reaches 3940 GB/s of message
+# bytes (tools/microbench.hip compress_test "512 x 1024",
+# profiles/microbench_issue_r01.json), 97 % of this ceiling at 2.4 GHz.
 COMPRESS_ONLY_GBS = 3939.8
 CONSUMER_INSTR_PER_BLOCK = 427.75
 ROUND_VALU_PER_BLOCK = 400
-FUSED_SIMD_CYCLES_PER_BLOCK = 2043.5
+FUSED_VALU_PER_BLOCK = 621.75
+FUSED_SIMD_CYCLES_PER_BLOCK = FUSED_VALU_PER_BLOCK * 4.0
 ISSUE_CYCLES = 4.0
 CLOCK_HZ = 2.4e9  # MI355X max engine clock; the chip holds it at config-2 occupancy
 SIMDS_PER_CU = 4
@@ -241,9 +244,9 @@ def main():
             "floor_ms": round(floor_ms, 4), "achieved_ms": round(kern_ms, 4),
             "frac": round(floor_ms / kern_ms, 4),
             "model": f"{waves_per_simd:g} waves/SIMD x {blocks} blocks x "
-                     f"{FUSED_SIMD_CYCLES_PER_BLOCK} SIMD cycles / 2.4 GHz (400 half-rate x 4 + "
-                     "221.75 full-rate x 2 per block, profiles/isa_mix_r02.json); the chip "
-                     "holds ~2.05 GHz under this load (profiles/pmc_fused_131072_r01.json)",
+                     f"{FUSED_SIMD_CYCLES_PER_BLOCK:g} SIMD cycles / 2.4 GHz ({FUSED_VALU_PER_BLOCK} VALU "
+                     "per block x 4 cycles, profiles/isa_mix_r02.json); the chip holds "
+                     "~2.2 GHz under this load (profiles/pmc_shape_r03.json)",
         }
     else:  # forced lane kernel, 1-block or A/B split shapes: not modelled
         binding = {"limit": "not modelled", "kernel": regime, "achieved_ms": round(kern_ms, 4)}
@@ -284,7 +287,7 @@ def main():
             "achieved": round(achieved, 2), "peak": round(valu_peak, 1), "unit": "GB/s",
             "frac": round(achieved / valu_peak, 4),
             "model": f"{cus * SIMDS_PER_CU} SIMDs x 64 chunks x 64 B per "
-                     f"{FUSED_SIMD_CYCLES_PER_BLOCK} SIMD cycles at 2.4 GHz",
+                     f"{FUSED_SIMD_CYCLES_PER_BLOCK:g} SIMD cycles (621.75 VALU x 4) at 2.4 GHz",
             "measured_compress_only": COMPRESS_ONLY_GBS,
             "frac_of_measured": round(achieved / COMPRESS_ONLY_GBS, 4),
         },
