@@ -66,6 +66,7 @@ for s in $STEPS; do
     vqbench) run vqbench 600 python tools/vq_bench.py --chunks 16384 --batches 64,256,1024 --reps 3 \
                  --out "$OUT/vq_bench.json" ;;
     configs) run configs 900 python tools/bench_configs.py --out "$OUT/configs.json" ;;
+    pmcicache) for n in 4096 32768; do run pmcic_$n 400 bash tools/pmc_icache.sh "$OUT/pmcic_$n" $n; done ;;
     *) echo "unknown step $s" ;;
     esac
 done
