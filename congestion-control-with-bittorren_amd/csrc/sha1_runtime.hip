@@ -1171,8 +1171,13 @@ int vq_maybe_launch(sha1chunk_vq* q) {
 // No copy engine, no launch per batch: a chunk starts hashing as soon as
 // its group is published.  A group is published when it holds
 // min(batch, 64) chunks, or at once while fewer groups are in flight than
-// the device has CUs (so at low rates every chunk goes alone and comes back
-// after its own serial chain, ~6 ms for 512 KiB, whatever the batch size).
+// the drain has workgroups (so at low rates every chunk goes alone and comes
+// back after its own serial chain, ~6 ms for 512 KiB, whatever the batch
+// size).  The drain takes SHA1CHUNK_VQ_CUS CUs (default 64 of 256): the
+// queue is PCIe-bound (64 groups of 64 chunks in flight are far more than
+// the link feeds), and the rest of the GPU stays free for the process's
+// other kernels, which could not share a CU with a drain workgroup (it holds
+// the CU's whole LDS).
 // Positions in both rings are monotonic counters (physical = counter mod
 // ring size); a group never wraps either ring.
 constexpr uint32_t kPvqMaxGroup = 64;
@@ -1190,7 +1195,7 @@ struct PvqGroup {
     bool collected;
 };
 struct Pvq {
-    int dev = 0, cus = 256;
+    int dev = 0, cus = 256;  // cus: the drain's workgroups (one per CU)
     uint32_t nslots = 0;  // slot ring (chunks) = group ring entries
     uint64_t nbytes = 0;  // data ring bytes
     uint32_t maxlen = 0;
@@ -1348,7 +1353,8 @@ void pvq_destroy(Pvq* P) {
 Pvq* pvq_create(Device* D, size_t batch, uint32_t max_chunk_len) {
     auto* P = new Pvq();
     P->dev = D->id;
-    P->cus = std::min(D->cus, 1024);
+    P->cus = static_cast<int>(std::max<uint64_t>(
+        1, std::min<uint64_t>({static_cast<uint64_t>(D->cus), 1024, env_u64("SHA1CHUNK_VQ_CUS", 64)})));
     P->maxlen = max_chunk_len;
     P->group_max = static_cast<uint32_t>(std::min<size_t>(batch, kPvqMaxGroup));
     P->idle_ticks = env_u64("SHA1CHUNK_VQ_IDLE_MS", 20) * 100000ull;  // s_memrealtime: 100 MHz

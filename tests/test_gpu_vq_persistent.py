@@ -174,3 +174,34 @@ def test_small_chunks_many_groups(pkg, dev, persistent):
         secs = time.perf_counter() - t0
     print(f"persistent verify queue: {n} chunks of 0..8 KiB in {secs * 1e3:.0f} ms ({n / secs:.0f} chunks/s)")
     assert got == want
+
+
+def test_device_batches_run_beside_a_busy_drain(pkg, dev, persistent):
+    """The drain takes SHA1CHUNK_VQ_CUS (default 64) CUs, holding their LDS:
+    a device batch of the same process (config 2: 4096 x 512 KiB) still runs
+    while the queue is busy, and both give the right results."""
+    torch = dev
+    rng = np.random.default_rng(12)
+    pool = [rng.integers(0, 256, L512, dtype=np.uint8).tobytes() for _ in range(4)]
+    digs = [hashlib.sha1(b).digest() for b in pool]
+    n_dev = 4096
+    buf = torch.empty(n_dev * L512, dtype=torch.uint8, device="cuda")
+    pkg.synth_fill_device(buf, 0, n_dev, L512)
+    dig = torch.zeros((n_dev, 20), dtype=torch.uint8, device="cuda")
+    torch.cuda.synchronize()
+    want = np.fromfile(os.path.join(os.path.dirname(__file__), "golden", "synth_4096x512k.bin"),
+                       np.uint8).reshape(-1, 20)
+    got = {}
+    with pkg.VerifyQueue(batch=64, max_chunk_len=L512) as q:
+        for t in range(1024):  # keeps the drain busy for a while
+            q.submit(pool[t % 4], digs[t % 4], t)
+        t0 = time.perf_counter()
+        pkg.hash_uniform_device(buf, L512, n_dev, dig)
+        torch.cuda.synchronize()
+        dev_s = time.perf_counter() - t0
+        for tag, m in q.poll(wait=True, max_results=1 << 16):
+            got[tag] = m
+    print(f"config-2 batch beside a busy verify drain: {dev_s * 1e3:.1f} ms")
+    assert got == {t: 0 for t in range(1024)}
+    assert np.array_equal(dig.cpu().numpy(), want)
+    assert dev_s < 5.0
