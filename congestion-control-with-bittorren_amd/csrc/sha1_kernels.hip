@@ -1228,8 +1228,8 @@ __global__ __launch_bounds__(kMixedThreads) void sha1_mixed_persistent_kernel(Ba
 // cached), wave 0 compares the 64 digests with the expected ones and
 // writes a 0/1 per chunk and the group's completion word to host memory.
 // Without work a workgroup sleeps (exponential backoff up to ~50 us) and
-// exits after `idle_ticks` of 100 MHz time, or at once when the host sets
-// `stop`.  Exit handshake (no lost group): the workgroup clears its alive
+// exits once no group has been claimed for `idle_ticks` of 100 MHz time, or
+// at once when the host sets `stop`.  Exit handshake (no lost group): the workgroup clears its alive
 // word, fences, and re-reads `pub`; the host stores `pub`, fences, and reads
 // the alive words.  At least one of them sees the other: either the
 // workgroup claims the new group or the host launches a new drain.
@@ -1242,18 +1242,28 @@ __device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// Lane 0 only: a claimed group index, kVqIdle or kVqExit.
-__device__ uint32_t vq_next(const VqDrainArgs& Q, uint64_t last_work) {
+// Lane 0 only: a claimed group index, kVqIdle or kVqExit.  Idleness is the
+// queue's, not the workgroup's: `last` is when the claim counter last moved
+// (any workgroup's claim), so under load no workgroup leaves, and after a
+// quiet spell the drain's workgroups leave together.
+__device__ uint32_t vq_next(const VqDrainArgs& Q, uint64_t& last, uint32_t& seen) {
     for (int round = 0; round < 2; ++round) {
         uint32_t p = ld_sys(Q.pub);
         uint32_t c = __hip_atomic_load(Q.claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (c != seen) {
+            seen = c;
+            last = __builtin_amdgcn_s_memrealtime();
+        }
         while (c < p) {
             if (__hip_atomic_compare_exchange_strong(Q.claim, &c, c + 1u, __ATOMIC_ACQ_REL, __ATOMIC_RELAXED,
-                                                     __HIP_MEMORY_SCOPE_AGENT))
+                                                     __HIP_MEMORY_SCOPE_AGENT)) {
+                seen = c + 1u;
+                last = __builtin_amdgcn_s_memrealtime();
                 return c;
+            }
         }
         if (ld_sys(Q.stop)) return kVqExit;
-        if (round == 1 || __builtin_amdgcn_s_memrealtime() - last_work <= Q.idle_ticks) return kVqIdle;
+        if (round == 1 || __builtin_amdgcn_s_memrealtime() - last <= Q.idle_ticks) return kVqIdle;
         // idle too long: leave, unless a group was published meanwhile
         st_sys(Q.alive + blockIdx.x, 0u);
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
@@ -1269,10 +1279,11 @@ __global__ __launch_bounds__(kMixedThreads) void sha1_vq_drain_kernel(VqDrainArg
     uint32_t* slot = reinterpret_cast<uint32_t*>(lds);  // free between jobs
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
-    uint64_t last_work = __builtin_amdgcn_s_memrealtime();
+    uint64_t last = __builtin_amdgcn_s_memrealtime();
+    uint32_t seen = 0xffffffffu;
     uint32_t backoff = 1;
     for (;;) {
-        if (threadIdx.x == 0) slot[0] = vq_next(Q, last_work);
+        if (threadIdx.x == 0) slot[0] = vq_next(Q, last, seen);
         __syncthreads();
         const uint32_t g = __builtin_amdgcn_readfirstlane(slot[0]);
         __syncthreads();  // every wave has the command before the LDS is reused
@@ -1312,7 +1323,6 @@ __global__ __launch_bounds__(kMixedThreads) void sha1_vq_drain_kernel(VqDrainArg
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
             if (lane == 0) st_sys(Q.done + gi, g + 1u);
         }
-        last_work = __builtin_amdgcn_s_memrealtime();
     }
 }
 

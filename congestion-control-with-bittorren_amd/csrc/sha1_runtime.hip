@@ -1185,7 +1185,7 @@ struct PvqCtl {
     uint32_t pub;   // groups published (host store, release)
     uint32_t stop;  // destroy: exit once nothing is claimable
     uint32_t pad[30];
-    uint32_t alive[1024];
+    uint32_t alive[2][1024];  // per launch slot, per workgroup
 };
 struct PvqGroup {
     uint64_t g;         // group index
@@ -1223,8 +1223,11 @@ struct Pvq {
     size_t inflight = 0;          // published, not yet collected
     std::deque<std::pair<uint64_t, uint8_t>> ready;
     size_t pending = 0;
+    // two launch slots, each a stream, an alive-word set and the event of
+    // its last drain; a slot is reused only once that drain has ended
     hipStream_t stream[2] = {nullptr, nullptr};
-    int next_stream = 0;
+    hipEvent_t ended[2] = {nullptr, nullptr};
+    bool launched[2] = {false, false};
     PartPool* copier = nullptr;
 };
 
@@ -1233,10 +1236,10 @@ uint64_t env_u64(const char* name, uint64_t dflt) {
     return e ? strtoull(e, nullptr, 10) : dflt;
 }
 
-int pvq_launch(Pvq* P) {
+int pvq_launch(Pvq* P, int k) {
     // every workgroup of the new drain counts as alive from here on, so a
     // submit right after does not launch another one
-    for (int w = 0; w < P->cus; ++w) __atomic_store_n(&P->ctl->alive[w], 1u, __ATOMIC_RELEASE);
+    for (int w = 0; w < P->cus; ++w) __atomic_store_n(&P->ctl->alive[k][w], 1u, __ATOMIC_RELEASE);
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
     VqDrainArgs Q{};
     Q.data = P->data;
@@ -1246,28 +1249,42 @@ int pvq_launch(Pvq* P) {
     Q.grp = P->grp;
     Q.pub = &P->ctl->pub;
     Q.stop = &P->ctl->stop;
-    Q.alive = P->ctl->alive;
+    Q.alive = P->ctl->alive[k];
     Q.res = P->res;
     Q.done = P->done;
     Q.dig = P->dmem;
     Q.claim = reinterpret_cast<uint32_t*>(P->dmem + 20ull * P->nslots);
     Q.grp_ring = P->nslots;
     Q.idle_ticks = P->idle_ticks;
-    const int k = P->next_stream;
-    P->next_stream ^= 1;  // a new drain may start while an old one is still leaving
     HIP_TRY(hipSetDevice(P->dev));
     hipError_t e = launch_vq_drain(Q, static_cast<uint32_t>(P->cus), P->stream[k]);
     if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "vq drain launch: %s", hipGetErrorString(e));
+    HIP_TRY(hipEventRecord(P->ended[k], P->stream[k]));
+    P->launched[k] = true;
     return SHA1CHUNK_OK;
 }
 
-// After `pub` moved: launch a drain unless some workgroup is still alive
-// (it then sees the new groups: the exit handshake in sha1_kernels.hip).
+// After `pub` moved (and while waiting): keep the drain at full strength.
+// Workgroups leave one by one when they find nothing to claim, each with
+// the exit handshake of sha1_kernels.hip (so no published group is ever
+// left without a live workgroup that sees it).  When fewer than the drain's
+// workgroups are alive, a new drain is launched on a slot whose previous
+// drain has ended; the leftovers of the old one keep working until idle.
 int pvq_ensure_drain(Pvq* P) {
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
-    for (int w = 0; w < P->cus; ++w)
-        if (__atomic_load_n(&P->ctl->alive[w], __ATOMIC_ACQUIRE)) return SHA1CHUNK_OK;
-    return pvq_launch(P);
+    int alive = 0;
+    for (int k = 0; k < 2; ++k)
+        for (int w = 0; w < P->cus; ++w) alive += __atomic_load_n(&P->ctl->alive[k][w], __ATOMIC_ACQUIRE) != 0;
+    if (alive >= P->cus) return SHA1CHUNK_OK;
+    for (int k = 0; k < 2; ++k) {
+        if (P->launched[k]) {
+            const hipError_t q = hipEventQuery(P->ended[k]);
+            if (q == hipErrorNotReady) continue;
+            if (q != hipSuccess) return fail(SHA1CHUNK_EHIP, "vq drain: %s", hipGetErrorString(q));
+        }
+        return pvq_launch(P, k);
+    }
+    return SHA1CHUNK_OK;  // both slots' drains still leaving: the next call launches
 }
 
 int pvq_publish(Pvq* P) {
@@ -1342,6 +1359,7 @@ void pvq_destroy(Pvq* P) {
     }
     for (int k = 0; k < 2; ++k) {
         if (P->stream[k]) (void)hipStreamSynchronize(P->stream[k]);
+        if (P->ended[k]) (void)hipEventDestroy(P->ended[k]);
         if (P->stream[k]) (void)hipStreamDestroy(P->stream[k]);
     }
     if (P->dmem) (void)hipFree(P->dmem);
@@ -1396,7 +1414,8 @@ Pvq* pvq_create(Device* D, size_t batch, uint32_t max_chunk_len) {
         return nullptr;
     }
     for (int k = 0; k < 2; ++k)
-        if (hipStreamCreateWithFlags(&P->stream[k], hipStreamNonBlocking) != hipSuccess) {
+        if (hipStreamCreateWithFlags(&P->stream[k], hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&P->ended[k], hipEventDisableTiming) != hipSuccess) {
             fail(SHA1CHUNK_EHIP, "vq: stream creation");
             pvq_destroy(P);
             return nullptr;
