@@ -137,9 +137,10 @@ int sha1chunk_synth_fill_ragged_async(void *d_base, const uint64_t *d_offsets,
  * Default: a persistent drain kernel.  The chunks go into a ring in pinned
  * host memory (SHA1CHUNK_VQ_RING_MIB, default 1024) and are published in
  * groups of up to min(batch, 64); while fewer groups are in flight than the
- * GPU has CUs, each chunk goes out at once.  One workgroup per CU pulls the
- * groups over PCIe, hashes and compares them, and writes the results back to
- * host memory; it exits after SHA1CHUNK_VQ_IDLE_MS (default 20) without work
+ * drain has workgroups, each chunk goes out at once.  The drain, one
+ * workgroup on each of SHA1CHUNK_VQ_CUS CUs (default 64), pulls the groups
+ * over PCIe, hashes and compares them, and writes the results back to host
+ * memory; it exits after SHA1CHUNK_VQ_IDLE_MS (default 20) without a claim
  * and the next submit starts it again.  A lone chunk comes back after its
  * own serial chain, with no batch to fill and no flush.
  *
@@ -155,8 +156,8 @@ int sha1chunk_synth_fill_ragged_async(void *d_base, const uint64_t *d_offsets,
  * Both: one queue per thread; queues on one device share nothing.  The copy
  * is split over SHA1CHUNK_VQ_THREADS threads (default 4, the caller
  * included: three helper threads per queue that spin briefly between
- * submissions).  Measured on 16384 x 512 KiB host chunks: 29-33 GiB/s
- * persistent, 26-37 GiB/s batch. */
+ * submissions).  Measured on 16384 x 512 KiB host chunks: 26-35 GiB/s
+ * persistent, 23-37 GiB/s batch. */
 typedef struct sha1chunk_vq sha1chunk_vq;
 /* NULL on failure (sha1chunk_last_error() says why). */
 sha1chunk_vq *sha1chunk_vq_create(size_t batch, uint32_t max_chunk_len);
