@@ -1164,9 +1164,10 @@ int vq_maybe_launch(sha1chunk_vq* q) {
 // host copies each submitted chunk into a ring in pinned, uncached host
 // memory, writes its length and expected digest next to it, and publishes
 // groups of up to 64 chunks by bumping `pub`.  The drain -- one workgroup
-// per CU, started when work is published and no workgroup is alive, gone
-// again after SHA1CHUNK_VQ_IDLE_MS (default 20) without work -- reads the
-// ring over PCIe, hashes each group in the one-group split shape and writes
+// per CU on SHA1CHUNK_VQ_CUS CUs, (re)launched whenever work is published
+// and fewer of its workgroups are alive than that, gone again after
+// SHA1CHUNK_VQ_IDLE_MS (default 20) without a claim -- reads the ring over
+// PCIe, hashes each group in the one-group split shape and writes
 // one 0/1 per chunk plus the group's completion word back to host memory.
 // No copy engine, no launch per batch: a chunk starts hashing as soon as
 // its group is published.  A group is published when it holds
