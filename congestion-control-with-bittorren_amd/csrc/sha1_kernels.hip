@@ -1229,10 +1229,11 @@ __global__ __launch_bounds__(kMixedThreads) void sha1_mixed_persistent_kernel(Ba
 // writes a 0/1 per chunk and the group's completion word to host memory.
 // Without work a workgroup sleeps (exponential backoff up to ~50 us) and
 // exits once no group has been claimed for `idle_ticks` of 100 MHz time, or
-// at once when the host sets `stop`.  Exit handshake (no lost group): the workgroup clears its alive
-// word, fences, and re-reads `pub`; the host stores `pub`, fences, and reads
-// the alive words.  At least one of them sees the other: either the
-// workgroup claims the new group or the host launches a new drain.
+// at once when the host sets `stop`.  Exit handshake (no lost group): the
+// workgroup clears its alive word, fences, and re-reads `pub`; the host
+// stores `pub`, fences, and reads the alive words.  At least one of them
+// sees the other: either the workgroup claims the new group or the host
+// launches a new drain.
 constexpr uint32_t kVqIdle = 0xffffffffu, kVqExit = 0xfffffffeu;
 
 __device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
