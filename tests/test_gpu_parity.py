@@ -367,6 +367,46 @@ def test_partial_wave_and_empty(pkg, dev, oracle, kernel):
     assert not empty.cpu().numpy().any()
 
 
+@pytest.mark.parametrize("chunk_len", [65, 1001, 4097])
+def test_uniform_odd_lengths_every_regime(pkg, dev, oracle, chunk_len):
+    """The make_chunks layout (chunk i at i * chunk_len, chunk.c:15-27) with a
+    length that is not a multiple of 16, so almost every chunk starts
+    misaligned: AUTO at one group per CU (4-wave split), two per CU (the
+    8-wave uniform shape, lane-per-chunk loads) and beyond (fused), plus each
+    forced kernel at the middle size."""
+    torch = dev
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    rng = np.random.default_rng(chunk_len)
+    for n, kernels in ((64 * cus - 3, ("auto",)), (128 * cus - 5, ("auto", "lane", "fused", "split")),
+                       (192 * cus + 17, ("auto",))):
+        host = rng.integers(0, 256, n * chunk_len, dtype=np.uint8)
+        want = oracle.hash_batch(host, np.arange(n, dtype=np.uint64) * chunk_len,
+                                 np.full(n, chunk_len, np.uint32))
+        buf = torch.from_numpy(host).cuda()
+        for k in kernels:
+            dig = torch.zeros((n, 20), dtype=torch.uint8, device="cuda")
+            pkg.hash_uniform_device(buf, chunk_len, n, dig, kernel=k)
+            torch.cuda.synchronize()
+            assert np.array_equal(dig.cpu().numpy(), want), (n, k)
+
+
+def test_chunk_past_4gib_bit_count(pkg, dev, oracle):
+    """One chunk of 2^29 + 55 bytes: its bit count (sha.c:529-558, the 64-bit
+    totalLength) needs 33 bits, so the high length word of the final block is
+    1.  Device (AUTO) and host batch paths; the chunk exceeds a host slot and
+    goes alone in a grown one."""
+    torch = dev
+    L = (1 << 29) + 55
+    host = np.random.default_rng(29).integers(0, 256, L, dtype=np.uint8)
+    want = oracle.hash_batch(host, np.zeros(1, np.uint64), np.array([L], np.uint32))[0].tobytes()
+    dig = torch.zeros((1, 20), dtype=torch.uint8, device="cuda")
+    pkg.hash_uniform_device(torch.from_numpy(host).cuda(), L, 1, dig)
+    torch.cuda.synchronize()
+    assert dig.cpu().numpy()[0].tobytes() == want
+    got = pkg.hash_batch(host, np.zeros(1, np.uint64), np.array([L], np.uint32))
+    assert got[0].tobytes() == want
+
+
 def test_zero_length_chunks_device(pkg, dev, golden):
     torch = dev
     n = 70
