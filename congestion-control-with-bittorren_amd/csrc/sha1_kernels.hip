@@ -722,7 +722,7 @@ __device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uin
     // Two producers for 2-block units (each owning one block per unit) were
     // measured slower at two groups per CU: 6 waves on 4 SIMDs put producers
     // on the consumers' SIMDs (profiles/split_2prod_sweep_r01.json).
-    static_assert(NPROD == 1 || (PAIRS == 1 && U == 2 * NPROD) ||
+    static_assert(NPROD == 1 || (PAIRS == 1 && (U == 2 * NPROD || U == NPROD)) ||
                       (PAIRS == 2 && U == NPROD && (V & kVLayout8) != 0),
                   "two producers: one stage (U = 4) or one block (U = 2, 8-wave layout) each per unit");
     int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -1664,7 +1664,8 @@ bool split_unit_built(int u) {
 #ifdef SHA1CHUNK_AB_VARIANTS
     static const int built[] = {1,  2,  3,  4,  8,  9,  10, 11, 12, 20, 21, 22, 23, 24, 26, 27,
                                 30, 31, 32, 33, 34, 36, 37, 42, 44, 45, 46, 504, 505, 506, 507,
-                                569, 577, 578, 579, 580, 581, 13, 583, 584, 585, 86, 87, 590, 14, 15};
+                                569, 577, 578, 579, 580, 581, 13, 583, 584, 585, 86, 87, 590, 14, 15,
+                                16, 17};
     for (int b : built)
         if (u == b) return true;
     return false;
@@ -1767,6 +1768,19 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     case 13:  // case 11 with lane-per-chunk producer loads (round-2 A/B of kVCoop)
         hipLaunchKernelGGL((sha1_split_kernel<2, 2, kSplit8V & ~kVCoop, 2>), dim3((groups + 1) / 2), dim3(512), 0,
                            st, A);
+        break;
+
+    // Round-3 A/B: one pair per workgroup with 2-block units and two producers
+    // (one block each per unit; waves 0, 1, 3 as in case 4): the config-2
+    // layout with case 11's unit size and 80 KiB of LDS.  Separates the cost
+    // of barriers every 2 blocks from that of two pairs sharing a CU.
+    case 16:
+        hipLaunchKernelGGL((sha1_split_kernel<2, 1, kVWK | kVUnmask | kVSkipWave2 | kVRead10 | kVCoop, 2>),
+                           dim3(groups), dim3(256), 0, st, A);
+        break;
+    case 17:  // case 16 with lane-per-chunk producer loads
+        hipLaunchKernelGGL((sha1_split_kernel<2, 1, kVWK | kVUnmask | kVSkipWave2 | kVRead10, 2>), dim3(groups),
+                           dim3(256), 0, st, A);
         break;
 
     case 8:  // 4 pairs per workgroup (512 threads), one consumer + producer per SIMD
