@@ -564,6 +564,12 @@ constexpr int kVSkipWave2 = 64;
 constexpr int kVLayout8 = 128;
 constexpr int kVSkipWave1 = 512;  // with kVSkipWave2: leave wave 1 empty instead of wave 2 (A/B)
 constexpr int kVCross = 256;
+// Round-3 A/B (A/B library only): the 8-wave layout with the consumers on
+// waves 0 and 1 (different halves of the LDS store path, SIMDs {0,1} / {2,3})
+// and the producers on waves 2 + 6 and 3 + 7 (waves 4, 5 empty), so each half
+// carries one consumer's reads and two producers' stores; with kVCross each
+// consumer's producers sit on the other half.
+constexpr int kVHalves = 32768;
 // Round-2 A/B flags (A/B library only): consumer at s_setprio 3; all 20
 // schedule reads of the next block in one burst before round 0.
 constexpr int kVPrio = 2048;
@@ -738,9 +744,15 @@ __device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uin
     uint32_t pidx = producer ? (uint32_t)(wave - PAIRS) / PAIRS : 0u;  // producer index
     if constexpr ((V & kVLayout8) != 0) {
         static_assert(PAIRS == 2 && NPROD == 2, "8-wave layout: two pairs, two producers each");
-        if (wave == 4 || wave == 6) return;  // never joins a barrier
-        producer = (wave & 1) != 0;
-        pair = producer ? (((wave >> 1) & 1) ^ ((V & kVCross) ? 1 : 0)) : (wave >> 1);
+        if constexpr ((V & kVHalves) != 0) {
+            if (wave == 4 || wave == 5) return;  // never joins a barrier
+            producer = wave >= 2;
+            pair = producer ? ((wave & 1) ^ ((V & kVCross) ? 1 : 0)) : wave;
+        } else {
+            if (wave == 4 || wave == 6) return;  // never joins a barrier
+            producer = (wave & 1) != 0;
+            pair = producer ? (((wave >> 1) & 1) ^ ((V & kVCross) ? 1 : 0)) : (wave >> 1);
+        }
         pidx = producer ? (uint32_t)(wave >> 2) : 0u;
     }
     const int lane = threadIdx.x & 63;
@@ -1665,7 +1677,7 @@ bool split_unit_built(int u) {
     static const int built[] = {1,  2,  3,  4,  8,  9,  10, 11, 12, 20, 21, 22, 23, 24, 26, 27,
                                 30, 31, 32, 33, 34, 36, 37, 42, 44, 45, 46, 504, 505, 506, 507,
                                 569, 577, 578, 579, 580, 581, 13, 583, 584, 585, 86, 87, 590, 14, 15,
-                                16, 17};
+                                16, 17, 18, 19};
     for (int b : built)
         if (u == b) return true;
     return false;
@@ -1781,6 +1793,17 @@ hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st) {
     case 17:  // case 16 with lane-per-chunk producer loads
         hipLaunchKernelGGL((sha1_split_kernel<2, 1, kVWK | kVUnmask | kVSkipWave2 | kVRead10, 2>), dim3(groups),
                            dim3(256), 0, st, A);
+        break;
+
+    // Round-3 A/B of the LDS store-path halves (kVHalves), lane-per-chunk
+    // producer loads as in the product's uniform case 11 (= case 13)
+    case 18:  // each consumer's producers on the other half
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, (kSplit8V & ~kVCoop) | kVHalves, 2>), dim3((groups + 1) / 2),
+                           dim3(512), 0, st, A);
+        break;
+    case 19:  // each consumer's producers on its own half
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, (kSplit8V & ~(kVCoop | kVCross)) | kVHalves, 2>),
+                           dim3((groups + 1) / 2), dim3(512), 0, st, A);
         break;
 
     case 8:  // 4 pairs per workgroup (512 threads), one consumer + producer per SIMD
