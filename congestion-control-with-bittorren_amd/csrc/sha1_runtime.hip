@@ -217,6 +217,12 @@ int ensure_slots(Device& D, int n) {
     return SHA1CHUNK_OK;
 }
 
+// The shared H2D stream of multi-slot pipelines (caller holds D.mu).
+int ensure_copy(Device& D) {
+    if (!D.copy) HIP_TRY(hipStreamCreateWithFlags(&D.copy, hipStreamNonBlocking));
+    return SHA1CHUNK_OK;
+}
+
 // Acquire the calling thread's device (initialising it on first use).
 int get_device(Device** out) {
     if (device_count() <= 0) return fail(SHA1CHUNK_ENODEV, "%s", g_probe_err.c_str());
@@ -229,13 +235,13 @@ int get_device(Device** out) {
             hipDeviceProp_t pr;
             HIP_TRY(hipGetDeviceProperties(&pr, D.id));
             D.cus = pr.multiProcessorCount;
-            // Only slot 0 and the copy stream now: a stream costs ~20 ms to
-            // create (profiles/startup_r01.json), and a one-chunk caller
-            // (shahash, verify_hash, the CLI on a small file) needs no more.
-            // Other slots are made by ensure_slots() on first use.
+            // Only slot 0 now: a stream costs ~12-20 ms to create
+            // (profiles/startup_r01.json, init_cost_r02.jsonl), and a caller
+            // whose batch fits one slot (shahash, verify_hash, the CLI on a
+            // small file) copies on that slot's own stream.  Other slots and
+            // the copy stream are made on first use (ensure_slots, ensure_copy).
             int rc = ensure_slots(D, 1);
             if (rc) return rc;
-            HIP_TRY(hipStreamCreateWithFlags(&D.copy, hipStreamNonBlocking));
             D.ready.store(true, std::memory_order_release);
         }
     }
@@ -382,9 +388,11 @@ size_t slot_bytes_for(uint64_t total) {
     return std::min(hi, std::max(lo, static_cast<size_t>(total / 4)));
 }
 
-// The slot's stream waits for its H2D copies, issued on the copy stream.
-int copies_issued(Device& D, Slot& s) {
-    HIP_TRY(hipEventRecord(s.copied, D.copy));
+// The slot's stream waits for its H2D copies, issued on stream `cs` (the
+// copy stream, or the slot's own stream for a batch of one fill).
+int copies_issued(Slot& s, hipStream_t cs) {
+    if (cs == s.stream) return SHA1CHUNK_OK;
+    HIP_TRY(hipEventRecord(s.copied, cs));
     HIP_TRY(hipStreamWaitEvent(s.stream, s.copied, 0));
     return SHA1CHUNK_OK;
 }
@@ -425,7 +433,7 @@ void pack_range(PartPool& pool, uint8_t* h, const uint64_t* hoff, const uint8_t*
 
 int stage_and_launch(Device& D, Slot& s, const uint8_t* base, const uint64_t* offsets,
                      const uint32_t* lengths, const std::vector<uint32_t>& order, size_t lo,
-                     size_t hi, size_t data_bytes, bool src_pinned) {
+                     size_t hi, size_t data_bytes, bool src_pinned, hipStream_t cs) {
     const size_t m = hi - lo;
     const size_t meta = round_up(m * (sizeof(uint64_t) + sizeof(uint32_t)), kAlign);
     int rc;
@@ -466,8 +474,8 @@ int stage_and_launch(Device& D, Slot& s, const uint8_t* base, const uint64_t* of
     }
     uint8_t* d = static_cast<uint8_t*>(s.dmem.p);
     if (direct) {
-        HIP_TRY(hipMemcpyAsync(d, h, meta, hipMemcpyHostToDevice, D.copy));
-        if (span) HIP_TRY(hipMemcpyAsync(d + meta, base + span0, span, hipMemcpyHostToDevice, D.copy));
+        HIP_TRY(hipMemcpyAsync(d, h, meta, hipMemcpyHostToDevice, cs));
+        if (span) HIP_TRY(hipMemcpyAsync(d + meta, base + span0, span, hipMemcpyHostToDevice, cs));
     } else {
         // pack in runs of ~64 MiB and start each run's H2D as soon as it is
         // packed, so the copy engine works while the rest is packed
@@ -482,12 +490,12 @@ int stage_and_launch(Device& D, Slot& s, const uint8_t* base, const uint64_t* of
             while (j1 < m && hoff[j1] - hoff[j0] < piece) ++j1;
             const size_t end = j1 < m ? hoff[j1] : cur;
             pack_range(*D.pack, h, hoff, base, offsets, lengths, s.ids, j0, j1, end - hoff[j0]);
-            HIP_TRY(hipMemcpyAsync(d + hoff[j0], h + hoff[j0], end - hoff[j0], hipMemcpyHostToDevice, D.copy));
+            HIP_TRY(hipMemcpyAsync(d + hoff[j0], h + hoff[j0], end - hoff[j0], hipMemcpyHostToDevice, cs));
             j0 = j1;
         }
-        HIP_TRY(hipMemcpyAsync(d, h, meta, hipMemcpyHostToDevice, D.copy));
+        HIP_TRY(hipMemcpyAsync(d, h, meta, hipMemcpyHostToDevice, cs));
     }
-    if ((rc = copies_issued(D, s))) return rc;
+    if ((rc = copies_issued(s, cs))) return rc;
     BatchArgs A{};
     A.base = d;
     A.off = reinterpret_cast<const uint64_t*>(d);
@@ -531,7 +539,6 @@ int hash_host(const uint8_t* base, const uint64_t* offsets, const uint32_t* leng
     if (rc) return rc;
     std::lock_guard<std::mutex> lk(D->mu);
     if ((rc = discard_in_flight(*D))) return rc;
-    if ((rc = ensure_slots(*D, 2))) return rc;
     // Longest first, so every wave of 64 gets near-equal lengths (a wave
     // runs as long as its longest lane); equal lengths keep caller order.
     std::vector<uint32_t> order(n);
@@ -552,9 +559,15 @@ int hash_host(const uint8_t* base, const uint64_t* offsets, const uint32_t* leng
             bytes += b;
             ++hi;
         }
+        // A batch that fits one slot (a single chunk from shahash /
+        // verify_hash) copies on slot 0's stream and creates no other stream;
+        // larger ones share the copy stream and alternate two slots.
+        const bool one_fill = lo == 0 && hi == n;
+        if (!one_fill && ((rc = ensure_slots(*D, 2)) || (rc = ensure_copy(*D)))) return rc;
         Slot& s = D->slot[which];
         if ((rc = drain(s, digests))) return rc;
-        if ((rc = stage_and_launch(*D, s, base, offsets, lengths, order, lo, hi, bytes, pinned)))
+        if ((rc = stage_and_launch(*D, s, base, offsets, lengths, order, lo, hi, bytes, pinned,
+                                   one_fill ? s.stream : D->copy)))
             return rc;
         lo = hi;
         which ^= 1;
@@ -757,13 +770,14 @@ long hash_stream_sized(sha1chunk_reader_fn reader, void* reader_ctx, sha1chunk_s
     std::lock_guard<std::mutex> lk(D->mu);
     if ((rc = discard_in_flight(*D))) return rc;
     const int nslots = stream_slots();
-    if ((rc = ensure_slots(*D, nslots))) return rc;
     size_t slot_bytes = stream_slot_bytes();
+    bool one_fill = false;  // a known size that fits one slot: slot 0 alone, copies on its stream
     if (size_hint) {
         const size_t L = SHA1CHUNK_CHUNK_LEN;
         const size_t whole = round_up(size_hint, L);
         const size_t spread = std::max(size_t(64) << 20, round_up(size_hint / nslots, L));
         slot_bytes = std::min({slot_bytes, whole, spread});
+        one_fill = whole <= slot_bytes;
     }
     const size_t per_slot = slot_bytes / SHA1CHUNK_CHUNK_LEN;  // 1024 chunks per 512 MiB
     const size_t meta = round_up(per_slot * 12, kAlign);
@@ -779,8 +793,13 @@ long hash_stream_sized(sha1chunk_reader_fn reader, void* reader_ctx, sha1chunk_s
     };
     int which = 0;
     bool eof = false;
-    while (!eof) {
+    for (size_t fill = 0; !eof; ++fill) {
+        // streams on first use; a reader that delivers more than size_hint
+        // leaves the one-fill path at its second slot
+        if (fill == 1) one_fill = false;
+        if ((rc = ensure_slots(*D, which + 1)) || (!one_fill && (rc = ensure_copy(*D)))) return rc;
         Slot& s = D->slot[which];
+        const hipStream_t cs = one_fill ? s.stream : D->copy;
         if ((rc = finish(which))) return rc;
         if ((rc = s.hpin.ensure(meta + slot_bytes)) || (rc = s.dmem.ensure(meta + slot_bytes)) ||
             (rc = s.hdig.ensure(per_slot * 20)) || (rc = s.ddig.ensure(per_slot * 20)))
@@ -804,7 +823,7 @@ long hash_stream_sized(sha1chunk_reader_fn reader, void* reader_ctx, sha1chunk_s
             got += r;
             if (got - sent >= piece && got < slot_bytes) {
                 HIP_TRY(hipMemcpyAsync(d + meta + sent, h + meta + sent, got - sent, hipMemcpyHostToDevice,
-                                       D->copy));
+                                       cs));
                 sent = got;
             }
         }
@@ -817,9 +836,9 @@ long hash_stream_sized(sha1chunk_reader_fn reader, void* reader_ctx, sha1chunk_s
             hlen[j] = static_cast<uint32_t>(
                 std::min<size_t>(SHA1CHUNK_CHUNK_LEN, got - j * SHA1CHUNK_CHUNK_LEN));
         }
-        HIP_TRY(hipMemcpyAsync(d + meta + sent, h + meta + sent, got - sent, hipMemcpyHostToDevice, D->copy));
-        HIP_TRY(hipMemcpyAsync(d, h, m * 12, hipMemcpyHostToDevice, D->copy));  // offsets + lengths
-        if ((rc = copies_issued(*D, s))) return rc;
+        HIP_TRY(hipMemcpyAsync(d + meta + sent, h + meta + sent, got - sent, hipMemcpyHostToDevice, cs));
+        HIP_TRY(hipMemcpyAsync(d, h, m * 12, hipMemcpyHostToDevice, cs));  // offsets + lengths
+        if ((rc = copies_issued(s, cs))) return rc;
         BatchArgs A{};
         A.base = d;
         A.off = reinterpret_cast<const uint64_t*>(d);

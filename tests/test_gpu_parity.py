@@ -179,6 +179,40 @@ def test_make_chunks_slot_ring_wraps(pkg, dev, tmp_path):
     assert r.stdout == "".join(f"{i} {h}\n" for i, h in enumerate(want))
 
 
+@pytest.mark.parametrize("hint_chunks", [0, 1, 2, 4, 64])
+def test_stream_pipeline_size_hints(pkg, dev, hint_chunks):
+    """sha1chunk_hash_stream_sized with a size hint that is absent (0), too
+    small (the reader delivers more: the one-slot path must hand over to the
+    copy stream and the other slots mid-call), exact (4 chunks: one fill on
+    slot 0's own stream, no other stream) or too large.  The reader returns
+    short reads of odd sizes; every digest is checked with hashlib and the
+    sink must see ascending, contiguous chunk indices (chunk.c:15-27 order)."""
+    import ctypes as C
+    import hashlib
+    size = 3 * L512 + 777
+    data = np.random.default_rng(hint_chunks + 7).integers(0, 256, size, dtype=np.uint8).tobytes()
+    want = [hashlib.sha1(data[i:i + L512]).digest() for i in range(0, size, L512)]
+    pos = [0]
+
+    def reader(ctx, dst, n):
+        k = min(n, size - pos[0], 100_003)
+        C.memmove(dst, data[pos[0]:pos[0] + k], k)
+        pos[0] += k
+        return k
+
+    got, firsts = [], []
+
+    def sink(ctx, first, dig, count):  # (an assert here would not propagate through ctypes)
+        firsts.append((first, len(got)))
+        got.extend(bytes(dig[20 * j:20 * (j + 1)]) for j in range(count))
+
+    rf, sf = pkg.sha1chunk.READER_FN(reader), pkg.sha1chunk.SINK_FN(sink)
+    n = pkg.lib().sha1chunk_hash_stream_sized(rf, None, sf, None, hint_chunks * L512)
+    assert n == len(want), pkg.lib().sha1chunk_last_error()
+    assert all(f == k for f, k in firsts), firsts
+    assert got == want
+
+
 def test_reference_make_chunks_main_dropin(pkg, dev, golden, fixture_files, tmp_path):
     """The reference's own make_chunks.c main, unmodified, linked without
     chunk.o/sha.o against libsha1chunk.so (oracle/Makefile `dropin`, built in
