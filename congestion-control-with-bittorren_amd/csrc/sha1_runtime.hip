@@ -941,6 +941,68 @@ static void fd_sink(void* ctx, size_t first, const uint8_t* dig, size_t count) {
 }
 }  // namespace
 
+namespace {
+// SHA1CHUNK_FILE_DEVICES (make_chunks on a regular file): how many devices
+// share the file -- "all", or a count (default 1).  Each device hashes a
+// contiguous, chunk-aligned byte range with its own pread pool, host thread
+// and pipeline; digests land in disjoint slices of the caller's array (the
+// chunk list split per device, SURVEY.md 8e: no collective).
+int file_devices(uint64_t bytes) {
+    const char* e = getenv("SHA1CHUNK_FILE_DEVICES");
+    const int nd = device_count();
+    if (!e || nd <= 1) return 1;
+    const int want = strcmp(e, "all") == 0 ? nd : std::max(1, std::min(nd, atoi(e)));
+    // at least one chunk per device
+    const uint64_t chunks = (bytes + SHA1CHUNK_CHUNK_LEN - 1) / SHA1CHUNK_CHUNK_LEN;
+    return static_cast<int>(std::max<uint64_t>(1, std::min<uint64_t>(want, chunks)));
+}
+
+long hash_file_devices(int fd, off_t pos, off_t end, int nd, int read_threads, FdSink* sk) {
+    const uint64_t L = SHA1CHUNK_CHUNK_LEN;
+    const uint64_t chunks = (static_cast<uint64_t>(end - pos) + L - 1) / L;
+    std::vector<long> got(nd, 0);
+    std::vector<off_t> stop(nd, 0);
+    std::vector<std::string> errs(nd);
+    std::vector<std::thread> th;
+    const int caller_dev = t_dev;
+    for (int g = 0; g < nd; ++g) {
+        th.emplace_back([&, g] {
+            t_dev = (caller_dev + g) % device_count();
+            const uint64_t c0 = chunks * g / nd, c1 = chunks * (g + 1) / nd;
+            const off_t a = pos + static_cast<off_t>(c0 * L);
+            const off_t b = std::min(end, pos + static_cast<off_t>(c1 * L));
+            PartPool pool(std::max(1, read_threads) - 1);
+            ParFile f{fd, a, b, &pool};
+            struct Shift {
+                FdSink* sk;
+                uint64_t c0;
+            } sh{sk, c0};
+            auto sink = [](void* ctx, size_t first, const uint8_t* dig, size_t count) {
+                Shift* z = static_cast<Shift*>(ctx);
+                fd_sink(z->sk, z->c0 + first, dig, count);
+            };
+            got[g] = hash_stream_sized(par_reader, &f, sink, &sh, static_cast<uint64_t>(b - a));
+            stop[g] = f.pos;
+            if (got[g] < 0) errs[g] = t_err;
+        });
+    }
+    for (auto& t : th) t.join();
+    long n = 0;
+    for (int g = 0; g < nd; ++g) {
+        if (got[g] < 0) return fail(static_cast<int>(got[g]), "device %d: %s", g, errs[g].c_str());
+        const uint64_t c0 = chunks * g / nd, c1 = chunks * (g + 1) / nd;
+        n += got[g];
+        // a range that came up short (the file shrank) ends the file there
+        if (static_cast<uint64_t>(got[g]) < c1 - c0) {
+            (void)lseek(fd, stop[g], SEEK_SET);
+            return n;
+        }
+    }
+    (void)lseek(fd, stop[nd - 1], SEEK_SET);
+    return n;
+}
+}  // namespace
+
 long sha1chunk_hash_fd(int fd, uint8_t* digests, size_t max_chunks, size_t* total_chunks) {
     FdSink sk{digests, max_chunks};
     struct stat st;
@@ -948,10 +1010,17 @@ long sha1chunk_hash_fd(int fd, uint8_t* digests, size_t max_chunks, size_t* tota
     long n;
     if (fstat(fd, &st) == 0 && S_ISREG(st.st_mode) && pos >= 0) {
         const char* e = getenv("SHA1CHUNK_READ_THREADS");
-        PartPool pool((e ? std::max(1, atoi(e)) : 8) - 1);
-        ParFile f{fd, pos, std::max(pos, st.st_size), &pool};
-        n = hash_stream_sized(par_reader, &f, fd_sink, &sk, static_cast<uint64_t>(f.end - f.pos));
-        (void)lseek(fd, f.pos, SEEK_SET);
+        const int read_threads = e ? std::max(1, atoi(e)) : 8;
+        const off_t end = std::max(pos, st.st_size);
+        const int nd = file_devices(static_cast<uint64_t>(end - pos));
+        if (nd > 1) {
+            n = hash_file_devices(fd, pos, end, nd, read_threads, &sk);
+        } else {
+            PartPool pool(read_threads - 1);
+            ParFile f{fd, pos, end, &pool};
+            n = hash_stream_sized(par_reader, &f, fd_sink, &sk, static_cast<uint64_t>(f.end - f.pos));
+            (void)lseek(fd, f.pos, SEEK_SET);
+        }
     } else {
         n = sha1chunk_hash_stream(fd_reader, &fd, fd_sink, &sk);
     }

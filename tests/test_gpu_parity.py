@@ -179,6 +179,42 @@ def test_make_chunks_slot_ring_wraps(pkg, dev, tmp_path):
     assert r.stdout == "".join(f"{i} {h}\n" for i, h in enumerate(want))
 
 
+@pytest.mark.parametrize("size,skip", [(100 * 2**20 + 12345, 0), (2 * L512 - 3, 0), (7 * L512 + 9, L512 + 5)])
+def test_make_chunks_file_over_devices(pkg, dev, tmp_path, size, skip):
+    """make_chunks on a regular file split over devices
+    (SHA1CHUNK_FILE_DEVICES=all; SHA1CHUNK_VIRTUAL_DEVICES=3 gives three
+    logical devices, each with its own pread pool, thread and pipeline, over
+    the one GPU of the test box): contiguous chunk-aligned byte ranges, the
+    digests in one array in file order.  A 201-chunk file with 16 MiB slots
+    (every device's ring wraps), a 2-chunk file (fewer chunks than devices),
+    and a stream opened part-way in (chunks start at the stream position,
+    chunk.c:15-27 reads from where the FILE* is).  Through make_chunks in a
+    fresh process and through the make-chunks CLI; every digest against
+    hashlib."""
+    import hashlib
+    data = np.random.default_rng(size).integers(0, 256, size, dtype=np.uint8).tobytes()
+    p = tmp_path / "multi.bin"
+    p.write_bytes(data)
+    want = [hashlib.sha1(data[i:i + L512]).hexdigest() for i in range(skip, size, L512)]
+    env = dict(os.environ, SHA1CHUNK_VIRTUAL_DEVICES="3", SHA1CHUNK_FILE_DEVICES="all",
+               SHA1CHUNK_STREAM_SLOT_MIB="16", SHA1CHUNK_STREAM_PIECE_MIB="4")
+    code = ("import importlib, sys; m = importlib.import_module('congestion-control-with-bittorren_amd'); "
+            "m.set_device(0); f = open(sys.argv[1], 'rb'); f.seek(int(sys.argv[2])); "
+            "import os; d = m.make_chunks(f); print(os.lseek(f.fileno(), 0, os.SEEK_CUR)); "
+            "print('\\n'.join(x.hex() for x in d))")
+    r = subprocess.run([sys.executable, "-c", code, str(p), str(skip)], capture_output=True, text=True,
+                       env=env, cwd=ROOT, timeout=120)
+    assert r.returncode == 0, r.stderr
+    lines = r.stdout.split()
+    assert int(lines[0]) == size  # the stream is left at the end, as a read() loop leaves it
+    assert lines[1:] == want
+    if skip == 0:
+        r = subprocess.run([os.path.join(PKG_DIR, "make-chunks"), str(p)], capture_output=True,
+                           text=True, env=env, timeout=120)
+        assert r.returncode == 0, r.stderr
+        assert r.stdout == "".join(f"{i} {h}\n" for i, h in enumerate(want))
+
+
 @pytest.mark.parametrize("hint_chunks", [0, 1, 2, 4, 64])
 def test_stream_pipeline_size_hints(pkg, dev, hint_chunks):
     """sha1chunk_hash_stream_sized with a size hint that is absent (0), too
