@@ -186,23 +186,29 @@ int main(void) {
         free(doff), free(dlen), free(hb), free(want), free(gotd);
     }
 
-    /* file pipeline: make_chunks(FILE*) and the fd path over a temp file */
+    /* file pipeline: make_chunks(FILE*) and the fd path over a temp file, on
+     * one device and split over every device (SHA1CHUNK_FILE_DEVICES; the
+     * test runs the driver with SHA1CHUNK_VIRTUAL_DEVICES=2) */
     char path[] = "/tmp/asan_driver_XXXXXX";
     int fd = mkstemp(path);
     const size_t fbytes = 9 * (size_t)L512 + 12345;
     CHECK(fd >= 0 && write(fd, buf, fbytes) == (ssize_t)fbytes, "temp file");
     close(fd);
-    FILE *f = fopen(path, "r");
-    uint8_t *hs[10];
-    for (int i = 0; i < 10; ++i) hs[i] = malloc(20);
-    int m = make_chunks(f, hs);
-    fclose(f);
-    CHECK(m == 10, "make_chunks count %d", m);
-    for (int i = 0; i < 10 && i < m; ++i) {
-        shahash(buf + (size_t)i * L512, i < 9 ? (int)L512 : 12345, d);
-        CHECK(!memcmp(d, hs[i], 20), "make_chunks chunk %d", i);
-        free(hs[i]);
+    for (int fdv = 0; fdv < 2; ++fdv) {
+        if (fdv) setenv("SHA1CHUNK_FILE_DEVICES", "all", 1);
+        FILE *f = fopen(path, "r");
+        uint8_t *hs[10];
+        for (int i = 0; i < 10; ++i) hs[i] = malloc(20);
+        int m = make_chunks(f, hs);
+        fclose(f);
+        CHECK(m == 10, "make_chunks count %d (file devices: %d)", m, fdv);
+        for (int i = 0; i < 10; ++i) {
+            shahash(buf + (size_t)i * L512, i < 9 ? (int)L512 : 12345, d);
+            CHECK(i >= m || !memcmp(d, hs[i], 20), "make_chunks chunk %d (file devices: %d)", i, fdv);
+            free(hs[i]);
+        }
     }
+    unsetenv("SHA1CHUNK_FILE_DEVICES");
     char *hex = get_chunk_hash((char *)buf, L512);
     char want_hex[41];
     shahash(buf, L512, d);

@@ -557,7 +557,8 @@ def test_host_batch_all_devices(pkg, dev, oracle, golden):
 # ------------------------------------------------------- verify queue ----
 def test_host_paths_under_asan(pkg, dev):
     """Every host path of the library (batch pipelines, pinned staging, part
-    pools, verify queue with growth, streaming trio, make_chunks(FILE*),
+    pools, verify queue with growth, streaming trio, make_chunks(FILE*) on one
+    and on two (virtual) devices,
     get_chunk_hash/verify_hash, the device ragged path's sort and mixed-kernel
     planning with forced and malformed plans) under host AddressSanitizer + UBSan
     (`make asan`: csrc/asan_driver.c against build-asan/libsha1chunk.so,
@@ -566,7 +567,8 @@ def test_host_paths_under_asan(pkg, dev):
     exe = os.path.join(PKG_DIR, "build-asan", "asan_driver")
     assert os.path.exists(exe), "run `make -C congestion-control-with-bittorren_amd asan` first"
     env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:halt_on_error=1",
-               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1",
+               SHA1CHUNK_VIRTUAL_DEVICES="2")  # make_chunks split over two devices too
     r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=120)
     assert r.returncode == 0 and "asan-driver ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
 
