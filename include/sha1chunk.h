@@ -104,7 +104,12 @@ long sha1chunk_hash_stream(sha1chunk_reader_fn reader, void *reader_ctx, sha1chu
 long sha1chunk_hash_stream_sized(sha1chunk_reader_fn reader, void *reader_ctx,
                                  sha1chunk_sink_fn sink, void *sink_ctx, uint64_t size_hint);
 /* File-descriptor convenience: up to max_chunks digests into `digests`;
- * *total_chunks (optional) gets the file's chunk count. */
+ * *total_chunks (optional) gets the file's chunk count.  Hashes from the
+ * fd's current offset and leaves it at the end of what was read.  A regular
+ * file is read with parallel pread; with SHA1CHUNK_FILE_DEVICES=all (or a
+ * count) in the environment it is split into contiguous chunk-aligned ranges
+ * over that many devices, one pipeline each (make_chunks and the
+ * make-chunks CLI go through here). */
 long sha1chunk_hash_fd(int fd, uint8_t *digests, size_t max_chunks, size_t *total_chunks);
 
 /* Streaming support for SHA1Update/SHA1Final: compress nblocks whole 64-byte
