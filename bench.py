@@ -379,7 +379,9 @@ def _strong_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden):
 def _latency_one_chunk(dev: int) -> dict:
     """verify_hash (job.c:217-228) on one 512 KiB chunk through the library in
     a child process: the first call (HIP start-up and stream creation
-    included) and the median of 20 warm calls."""
+    included) and the median of 20 warm calls; then the same with the
+    opt-in host small-call path (SHA1CHUNK_HOST_SMALL=524288: the chunk is
+    hashed on the host, csrc/sha1_host.c, the device still required)."""
     import subprocess
     code = (
         "import ctypes, hashlib, json, os, sys, time\n"
@@ -404,13 +406,19 @@ def _latency_one_chunk(dev: int) -> dict:
         "print('LATENCY ' + json.dumps({'probe_ms': (t1 - t0) * 1e3, 'first_call_ms': (t2 - t1) * 1e3,\n"
         "      'warm_ms': float(np.median(warm)) * 1e3, 'warm_min_ms': min(warm) * 1e3}))\n")
     libp = os.path.join(ROOT, "congestion-control-with-bittorren_amd", "libsha1chunk.so")
-    try:
+
+    def child(extra_env):
+        env = dict(os.environ, **extra_env)
         r = subprocess.run([sys.executable, "-c", code, libp, str(dev)], capture_output=True,
-                           text=True, timeout=120)
+                           text=True, timeout=120, env=env)
         line = [x for x in r.stdout.splitlines() if x.startswith("LATENCY ")]
         if r.returncode != 0 or not line:
-            return {"error": (r.stderr or r.stdout)[-300:]}
-        d = json.loads(line[-1][8:])
+            raise RuntimeError((r.stderr or r.stdout)[-300:])
+        return json.loads(line[-1][8:])
+
+    try:
+        d = child({})
+        hs = child({"SHA1CHUNK_HOST_SMALL": str(CHUNK_LEN)})
     except Exception as e:  # a failed probe must not cost the bench line
         return {"error": repr(e)[:300]}
     return {"path": "verify_hash -> get_chunk_hash -> shahash -> sha1chunk_hash_batch(n=1): "
@@ -418,7 +426,12 @@ def _latency_one_chunk(dev: int) -> dict:
             "cold_ms": round(d["probe_ms"] + d["first_call_ms"], 3),
             "cold_first_call_ms": round(d["first_call_ms"], 3),
             "warm_ms": round(d["warm_ms"], 3), "warm_min_ms": round(d["warm_min_ms"], 3),
-            "bytes": CHUNK_LEN}
+            "bytes": CHUNK_LEN,
+            "host_small": {"knob": f"SHA1CHUNK_HOST_SMALL={CHUNK_LEN} (opt-in; off by default)",
+                           "path": "shahash on the host (csrc/sha1_host.c, x86 SHA extensions); "
+                                   "a device is still required",
+                           "cold_first_call_ms": round(hs["first_call_ms"], 3),
+                           "warm_ms": round(hs["warm_ms"], 3), "warm_min_ms": round(hs["warm_min_ms"], 3)}}
 
 
 def _traffic(n: int, L: int):

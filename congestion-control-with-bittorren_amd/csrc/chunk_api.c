@@ -11,10 +11,12 @@
  *   verify_chunk_hash                   chunk.c:204-217
  *   verify_hash                         job.c:217-228
  *
- * Every SHA-1 compression goes to the device.  The reference reports
- * failures by printing and exit(-1) (chunk.c:171-178); these void functions
- * do the same when the engine fails (no device, HIP error), so a missing GPU
- * is loud, never a silent CPU fallback.
+ * Every SHA-1 compression goes to the device (unless the process opts into
+ * SHA1CHUNK_HOST_SMALL, which hashes calls up to that size on the host and
+ * still requires the device; sha1_runtime.hip, sha1_host.c).  The reference
+ * reports failures by printing and exit(-1) (chunk.c:171-178); these void
+ * functions do the same when the engine fails (no device, HIP error), so a
+ * missing GPU is loud, never a silent CPU fallback.
  */
 #include <ctype.h>
 #include <pthread.h>

@@ -30,6 +30,7 @@
 
 #include "../../include/sha1chunk.h"
 #include "part_pool.hpp"
+#include "sha1_host.h"
 #include "sha1_kernels.h"
 
 namespace {
@@ -223,6 +224,21 @@ int ensure_copy(Device& D) {
     return SHA1CHUNK_OK;
 }
 
+// SHA1CHUNK_HOST_SMALL=<bytes> (default 0: off): host calls of at most that
+// many bytes -- one chunk from shahash / get_chunk_hash / verify_hash, the
+// streaming trio's updates -- are hashed on the host (sha1_host.c: x86 SHA
+// extensions) instead of as one lane's 6 ms serial chain on the device.
+// Opt-in for latency-bound single-chunk callers (SURVEY.md 7.1 step 2, 8f
+// rank 2); a device is still required, so this is never a fallback.
+uint64_t host_small_bytes() {
+    static const uint64_t b = [] {
+        const char* e = getenv("SHA1CHUNK_HOST_SMALL");
+        return e ? strtoull(e, nullptr, 10) : 0ull;
+    }();
+    return b;
+}
+int require_device();
+
 // Acquire the calling thread's device (initialising it on first use).
 int get_device(Device** out) {
     if (device_count() <= 0) return fail(SHA1CHUNK_ENODEV, "%s", g_probe_err.c_str());
@@ -246,6 +262,14 @@ int get_device(Device** out) {
         }
     }
     *out = &D;
+    return SHA1CHUNK_OK;
+}
+
+// The library's contract for every call, host small-call path included: a
+// gfx950 device is present and the thread's device index is valid.
+int require_device() {
+    if (device_count() <= 0) return fail(SHA1CHUNK_ENODEV, "%s", g_probe_err.c_str());
+    if (t_dev < 0 || t_dev >= g_count) return fail(SHA1CHUNK_EINVAL, "bad device %d", t_dev);
     return SHA1CHUNK_OK;
 }
 
@@ -709,6 +733,16 @@ int sha1chunk_hash_batch(const void* base, const uint64_t* offsets, const uint32
     if (n == 0) return SHA1CHUNK_OK;
     if (!base || !offsets || !lengths || !digests) return fail(SHA1CHUNK_EINVAL, "null pointer");
     if (n > 0xffffffffu) return fail(SHA1CHUNK_EINVAL, "n too large");
+    if (!(flags & SHA1CHUNK_DEVICE) && host_small_bytes()) {
+        uint64_t total = 0;
+        for (size_t i = 0; i < n && total <= host_small_bytes(); ++i) total += lengths[i];
+        if (total <= host_small_bytes()) {
+            if (int rc = require_device()) return rc;
+            const uint8_t* b = static_cast<const uint8_t*>(base);
+            for (size_t i = 0; i < n; ++i) sha1host_digest(b + offsets[i], lengths[i], digests + 20 * i);
+            return SHA1CHUNK_OK;
+        }
+    }
     if (flags & SHA1CHUNK_DEVICE) {
         Device* D;
         int rc = get_device(&D);
@@ -1033,6 +1067,11 @@ int sha1chunk_compress_blocks(uint32_t state[5], const void* blocks, size_t nblo
     if (!state || (nblocks && !blocks)) return fail(SHA1CHUNK_EINVAL, "null pointer");
     if (nblocks == 0) return SHA1CHUNK_OK;
     if (nblocks * 64 > 0xffffffffull) return fail(SHA1CHUNK_EINVAL, "too many blocks");
+    if (nblocks * 64 <= host_small_bytes()) {
+        if (int rc = require_device()) return rc;
+        sha1host_compress(state, blocks, nblocks);
+        return SHA1CHUNK_OK;
+    }
     Device* D;
     int rc = get_device(&D);
     if (rc) return rc;
@@ -1062,6 +1101,11 @@ int sha1chunk_finish(const uint32_t state[5], uint64_t prefix_bytes, const void*
                      uint32_t tail_len, uint8_t digest[20]) {
     if (!state || !digest || (tail_len && !tail) || tail_len >= 64)
         return fail(SHA1CHUNK_EINVAL, "bad argument");
+    if (host_small_bytes()) {
+        if (int rc = require_device()) return rc;
+        sha1host_finish(state, prefix_bytes, tail, tail_len, digest);
+        return SHA1CHUNK_OK;
+    }
     Device* D;
     int rc = get_device(&D);
     if (rc) return rc;

@@ -12,8 +12,9 @@ error behaviour; file:line into /root/reference):
     SHA1()  .init/.update/.final    sha.h:58-60      streaming context
 
 plus the batch / device entry points of include/sha1chunk.h that replace a
-loop of shahash() calls.  Every digest is computed by the gfx950 HIP kernels;
-there is no CPU path.  The library must have been built (`make -C
+loop of shahash() calls.  Every digest is computed by the gfx950 HIP kernels
+(unless the process opts into SHA1CHUNK_HOST_SMALL for small calls, which
+still needs the device); there is no CPU fallback.  The library must have been built (`make -C
 congestion-control-with-bittorren_amd` or __graft_entry__.build()); a missing
 library or device raises, it never falls back.
 

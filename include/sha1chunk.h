@@ -11,8 +11,14 @@
  *
  * Error convention: 0 on success, a negative SHA1CHUNK_E* code otherwise
  * (never exit()); sha1chunk_last_error() returns a thread-local message.
- * There is no CPU hashing path: without a usable gfx950 device every call
- * fails with SHA1CHUNK_ENODEV.
+ * There is no CPU fallback: without a usable gfx950 device every call
+ * fails with SHA1CHUNK_ENODEV.  Opt-in (off by default): with
+ * SHA1CHUNK_HOST_SMALL=<bytes> in the environment, host calls of at most
+ * that many bytes (sha1chunk_hash_batch / verify_batch on host memory,
+ * compress_blocks, finish: shahash, get_chunk_hash, verify_hash, the
+ * SHA1Update trio) are hashed on the host (x86 SHA extensions) -- one
+ * 512 KiB chunk in ~0.2 ms instead of one lane's ~6 ms serial chain -- and
+ * the device is still required.
  */
 #ifndef SHA1CHUNK_H
 #define SHA1CHUNK_H

@@ -571,6 +571,12 @@ def test_host_paths_under_asan(pkg, dev):
                SHA1CHUNK_VIRTUAL_DEVICES="2")  # make_chunks split over two devices too
     r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=120)
     assert r.returncode == 0 and "asan-driver ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
+    # again with the opt-in host small-call path (csrc/sha1_host.c under
+    # ASan/UBSan too): calls of <= 512 KiB hash on the host, so the driver's
+    # shahash-vs-make_chunks checks now compare host digests with device ones
+    env["SHA1CHUNK_HOST_SMALL"] = "524288"
+    r = subprocess.run([exe], capture_output=True, text=True, env=env, timeout=120)
+    assert r.returncode == 0 and "asan-driver ok" in r.stdout, (r.stdout[-1500:], r.stderr[-3000:])
 
 
 _ALL_DEVICES_SCRIPT = r"""
