@@ -137,11 +137,13 @@ __attribute__((target("sha,sse4.1,ssse3"))) static void compress_shani(uint32_t 
 
 static int use_shani(void) {
 #if defined(__x86_64__)
-    static int v = -1;
+    static int cached = -1;  /* decided once; racing first callers store the same value */
+    int v = __atomic_load_n(&cached, __ATOMIC_RELAXED);
     if (v < 0) {
         const char *p = getenv("SHA1HOST_PORTABLE");
         __builtin_cpu_init();
         v = !(p && atoi(p)) && __builtin_cpu_supports("sha") && __builtin_cpu_supports("sse4.1");
+        __atomic_store_n(&cached, v, __ATOMIC_RELAXED);
     }
     return v;
 #else
