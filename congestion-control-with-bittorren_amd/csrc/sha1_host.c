@@ -79,9 +79,10 @@ static void compress_portable(uint32_t h[5], const uint8_t *blocks, size_t nbloc
 #if defined(__x86_64__)
 #include <immintrin.h>
 
-/* Four rounds (function group G = 0..3) on message vector X (words t..t+3
- * in lanes 3..0).  E_IN is e (+ message) for the first step, later the
- * sha1nexte of the ABCD two steps back. */
+/* Four rounds 4I..4I+3 (function group G = 0..3) on message vector m[I&3]
+ * (words 4I..4I+3 in lanes 3..0).  Their e is the block's e for step 0,
+ * later rotl30 of the a that the previous step started from (sha1nexte of
+ * that step's input ABCD, `eprev`), added to the first word. */
 #define SHA1_STEP(I, G)                                                          \
     do {                                                                         \
         __m128i ein = (I) == 0 ? _mm_add_epi32(e, m[0]) : _mm_sha1nexte_epu32(eprev, m[(I)&3]); \
