@@ -128,6 +128,8 @@ def parse():
     ap.add_argument("--strong-total", type=int, default=262144,
                     help="chunks of the strong-scaling list (BASELINE config 4); 0 = skip")
     ap.add_argument("--strong-steps", type=int, default=10)
+    ap.add_argument("--weak4-chunks", type=int, default=65536,
+                    help="chunks per GPU of the config-4 weak-scaling leg (SURVEY.md 8d); 0 = skip")
     ap.add_argument("--no-latency", action="store_true")
     return ap.parse_args()
 
@@ -298,6 +300,8 @@ def main():
     torch.cuda.empty_cache()
     if a.strong_total > 0:
         result["strong"] = _strong_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden)
+    if a.weak4_chunks > 0:
+        result["weak_config4"] = _weak4_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden)
     if rank == 0 and world == 1 and not a.no_latency:
         result["latency_one_chunk"] = _latency_one_chunk(dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -374,6 +378,47 @@ def _strong_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden):
         dist.barrier()
     return shard.strong_report(total, L, world, ms_n, kern_ms, one_ms, one_kern_ms, parity,
                                one_parity, K)
+
+
+def _weak4_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden):
+    """Config 4's weak scaling (65536 chunks per GPU): every
+    rank hashes its own `per` chunks, no collective on the data path.  Rank r
+    takes shard r % 4 of the 4-way split of the config-4 list (for the
+    default 65536 chunks per rank), so its digest-of-digests has a reference
+    golden aggregate at any N; the bytes are the same synthetic chunks either
+    way.  Timed like the other legs (3 untimed launches, barrier + synchronize
+    around K, max over ranks)."""
+    per, L, K = a.weak4_chunks, CHUNK_LEN, max(1, a.strong_steps)
+    c4 = golden["config4"]
+    aggs4 = c4["shard_aggs"].get("4")
+    golden_ok = per * 4 == c4["chunks"] and aggs4 is not None
+    first = (rank % 4) * per if golden_ok else rank * per
+    st = torch.cuda.Stream()
+    buf = torch.empty(per * L, dtype=torch.uint8, device="cuda")
+    dig = torch.zeros((per, 20), dtype=torch.uint8, device="cuda")
+    pkg.synth_fill_device(buf, first, per, L, stream=st)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    wall, kern_ms = _time_launches(pkg, torch, buf, L, per, dig, st, K, 3)
+    if world > 1:
+        dist.barrier()
+    wall, kern_ms = shard.max_over_ranks([wall, kern_ms], device=cdev)
+    ok = golden_ok and hashlib.sha1(dig.cpu().numpy().tobytes()).hexdigest() == aggs4[rank % 4]
+    parity = shard.all_ranks_ok(ok, device=cdev)
+    del buf, dig
+    torch.cuda.empty_cache()
+    ms = wall / K * 1e3
+    return {
+        "workload": f"{per} x {L} B chunks per GPU, device-resident (config 4 weak scaling)",
+        "chunks_per_gpu": per, "n_gpus": world, "steps": K,
+        "ms_per_step": round(ms, 4), "kernel_ms": round(kern_ms, 4),
+        "value": round(world * per * L / 2**30 / (ms / 1e3), 2), "unit": "GiB/s",
+        "per_gpu_hbm_frac": round(per * (L + 20) / (kern_ms / 1e3) / (HBM_PEAK_GBS * 1e9), 5),
+        "kernel": _regime(per, 256, "auto"),
+        "parity": bool(parity),
+        "parity_ref": "each rank's digest-of-digests vs golden config4 shard_aggs[4][rank % 4]",
+    }
 
 
 def _latency_one_chunk(dev: int) -> dict:

@@ -1196,6 +1196,9 @@ struct Pvq;
 
 struct sha1chunk_vq {
     Pvq* pv = nullptr;  // the persistent drain (default), or null: batch launches (SHA1CHUNK_VQ_MODE=batch)
+    // batch size 1 with SHA1CHUNK_HOST_SMALL >= max_chunk_len: every submit
+    // is hashed and compared on the host at once (no sets, no drain)
+    bool host1 = false;
     int dev = 0;
     int cus = 256;
     size_t batch = 0;  // launch threshold
@@ -1625,6 +1628,19 @@ sha1chunk_vq* sha1chunk_vq_create(size_t batch, uint32_t max_chunk_len) {
         fail(SHA1CHUNK_EINVAL, "vq: batch 1..2^20 and max_chunk_len > 0 required");
         return nullptr;
     }
+    // The batch-size-1 host path ("keep the CPU path for
+    // batch size 1"): a peer verifying one chunk at a time, as
+    // packet_handler.c:472 -> job.c:217 does, would otherwise wait for one
+    // lane's serial chain (~6 ms per 512 KiB) per chunk.  Opt-in through the
+    // same knob as the other one-chunk calls; a device is still required.
+    if (batch == 1 && max_chunk_len <= host_small_bytes()) {
+        if (require_device()) return nullptr;
+        auto* q = new sha1chunk_vq();
+        q->host1 = true;
+        q->batch = q->cap = 1;
+        q->maxlen = max_chunk_len;
+        return q;
+    }
     Device* D;
     if (get_device(&D)) return nullptr;
     auto* q = new sha1chunk_vq();
@@ -1669,6 +1685,13 @@ int sha1chunk_vq_submit(sha1chunk_vq* q, const void* chunk, uint32_t len, const 
         return pvq_submit(q->pv, chunk, len, expected, tag);
     }
     if (len > q->maxlen) return fail(SHA1CHUNK_EINVAL, "vq: chunk of %u bytes > max %u", len, q->maxlen);
+    if (q->host1) {
+        uint8_t dig[20];
+        sha1host_digest(chunk, len, dig);
+        q->ready.emplace_back(tag, memcmp(dig, expected, 20) != 0 ? 1 : 0);
+        ++q->pending;
+        return SHA1CHUNK_OK;
+    }
     VqSet* S = &q->set[q->fill];
     while (S->inflight) {  // the fill set is still on the device: drain in order
         int rc = vq_collect_oldest(q);
@@ -1731,8 +1754,8 @@ size_t sha1chunk_vq_pending(const sha1chunk_vq* q) { return q ? (q->pv ? q->pv->
 
 void sha1chunk_vq_destroy(sha1chunk_vq* q) {
     if (!q) return;
-    if (q->pv) {
-        pvq_destroy(q->pv);
+    if (q->pv || q->host1) {
+        if (q->pv) pvq_destroy(q->pv);
         delete q;
         return;
     }

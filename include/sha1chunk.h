@@ -164,6 +164,12 @@ int sha1chunk_synth_fill_ragged_async(void *d_base, const uint64_t *d_offsets,
  * therefore always come back through poll() without a flush.  Three batch
  * sets are in flight at once.
  *
+ * batch == 1 with SHA1CHUNK_HOST_SMALL >= max_chunk_len (opt-in): the
+ * batch-size-1 host path.  Each submit hashes and compares its chunk on the
+ * host before returning (0.2 ms per 512 KiB instead of a 6 ms device chain);
+ * poll() returns the results in submission order.  A device is still
+ * required.
+ *
  * Both: one queue per thread; queues on one device share nothing.  The copy
  * is split over SHA1CHUNK_VQ_THREADS threads (default 4, the caller
  * included: three helper threads per queue that spin briefly between
