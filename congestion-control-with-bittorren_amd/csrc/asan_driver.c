@@ -99,13 +99,15 @@ int main(void) {
     /* verify queue, both implementations (batch launches; the persistent
      * drain reading a small pinned host ring, with a 1 ms idle exit so it
      * leaves and is relaunched): growth, polling, flush; every tag once with
-     * the right flag */
-    static const char *modes[2] = {"batch", "persistent"};
-    for (int mo = 0; mo < 2; ++mo) {
+     * the right flag.  The third pass is a batch-1 queue: the host path when
+     * SHA1CHUNK_HOST_SMALL covers L512, else the drain with one-chunk groups */
+    static const char *modes[3] = {"batch", "persistent", "persistent"};
+    static const size_t vq_batch[3] = {16, 16, 1};
+    for (int mo = 0; mo < 3; ++mo) {
     setenv("SHA1CHUNK_VQ_MODE", modes[mo], 1);
     setenv("SHA1CHUNK_VQ_IDLE_MS", "1", 1);
     setenv("SHA1CHUNK_VQ_RING_MIB", "8", 1);
-    sha1chunk_vq *q = sha1chunk_vq_create(16, L512);
+    sha1chunk_vq *q = sha1chunk_vq_create(vq_batch[mo], L512);
     CHECK(q != NULL, "vq_create: %s", sha1chunk_last_error());
     size_t seen = 0;
     uint8_t *got = calloc(n, 1);
