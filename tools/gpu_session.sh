@@ -65,6 +65,8 @@ for s in $STEPS; do
                    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 2 ;;
     vqbench) run vqbench 600 python tools/vq_bench.py --chunks 16384 --batches 64,256,1024 --reps 3 \
                  --out "$OUT/vq_bench.json" ;;
+    vqhost1) run vqhost1 300 python tools/vq_bench.py --chunks 4096 --batches 64 --reps 2 \
+                 --modes host1,persistent --out "$OUT/vq_host1.json" ;;
     configs) run configs 900 python tools/bench_configs.py --out "$OUT/configs.json" ;;
     pmcicache) for n in 4096 32768; do run pmcic_$n 400 bash tools/pmc_icache.sh "$OUT/pmcic_$n" $n; done ;;
     *) echo "unknown step $s" ;;
