@@ -34,6 +34,11 @@ time of the whole 262144-chunk list, measured on rank 0's GPU in the same run
 against the reference golden shard aggregate of the N-way split.
 `value` stays the weak config-2 number, so the N = 1 line is BENCH's.
 
+`weak_config4` (same line): config 4's weak scaling, 65536 chunks per GPU
+(SURVEY.md 8d), rank r hashing shard r mod 4 of the 4-way split of the
+config-4 list (shard.weak_golden_shard), checked against that shard's golden
+aggregate; timed like `strong`.
+
 `latency_one_chunk` (N = 1): the peer's synchronous receive-side verify,
 verify_hash() (job.c:217-228) on one 512 KiB chunk through the library, in a
 child process: cold (first call, HIP start-up included) and warm, next to the
@@ -390,9 +395,8 @@ def _weak4_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden):
     around K, max over ranks)."""
     per, L, K = a.weak4_chunks, CHUNK_LEN, max(1, a.strong_steps)
     c4 = golden["config4"]
-    aggs4 = c4["shard_aggs"].get("4")
-    golden_ok = per * 4 == c4["chunks"] and aggs4 is not None
-    first = (rank % 4) * per if golden_ok else rank * per
+    first, _, k_idx = shard.weak_golden_shard(rank, per, c4["chunks"])
+    aggs = c4["shard_aggs"].get(str(c4["chunks"] // per)) if k_idx is not None else None
     st = torch.cuda.Stream()
     buf = torch.empty(per * L, dtype=torch.uint8, device="cuda")
     dig = torch.zeros((per, 20), dtype=torch.uint8, device="cuda")
@@ -404,7 +408,7 @@ def _weak4_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden):
     if world > 1:
         dist.barrier()
     wall, kern_ms = shard.max_over_ranks([wall, kern_ms], device=cdev)
-    ok = golden_ok and hashlib.sha1(dig.cpu().numpy().tobytes()).hexdigest() == aggs4[rank % 4]
+    ok = aggs is not None and hashlib.sha1(dig.cpu().numpy().tobytes()).hexdigest() == aggs[k_idx]
     parity = shard.all_ranks_ok(ok, device=cdev)
     del buf, dig
     torch.cuda.empty_cache()
@@ -417,7 +421,8 @@ def _weak4_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden):
         "per_gpu_hbm_frac": round(per * (L + 20) / (kern_ms / 1e3) / (HBM_PEAK_GBS * 1e9), 5),
         "kernel": _regime(per, 256, "auto"),
         "parity": bool(parity),
-        "parity_ref": "each rank's digest-of-digests vs golden config4 shard_aggs[4][rank % 4]",
+        "parity_ref": "each rank's digest-of-digests vs golden config4 shard_aggs[k][rank % k], "
+                      "k = 262144 / chunks per GPU",
     }
 
 

@@ -26,6 +26,21 @@ def strong_shard(rank: int, world: int, total: int) -> tuple[int, int]:
     return first, base + (1 if rank < extra else 0)
 
 
+def weak_golden_shard(rank: int, per_rank: int, total: int) -> tuple[int, int, int | None]:
+    """Weak scaling over the ids of a fixed list of `total` chunks whose
+    k-way strong shards have golden aggregates (bench.py's config-4 weak leg:
+    65536 chunks per rank = one shard of the 4-way split of 262144): rank r
+    takes shard r mod k, k = total / per_rank, so every rank's bytes have a
+    reference digest-of-digests at any N.  Returns (first, count, shard
+    index), or the plain weak shard and None when per_rank does not divide
+    total."""
+    if per_rank <= 0 or total % per_rank:
+        return weak_shard(rank, per_rank) + (None,)
+    k = total // per_rank
+    first, count = strong_shard(rank % k, k, total)
+    return first, count, rank % k
+
+
 def strong_report(total: int, chunk_len: int, world: int, ms_n: float, kern_ms_n: float,
                   ms_1: float, kern_ms_1: float, parity: bool, parity_1: bool,
                   steps: int) -> dict:

@@ -126,3 +126,18 @@ def test_strong_and_byte_balanced_shards(pkg):
         cuts = shard.byte_balanced_cuts(lens, world)
         assert len(cuts) == world + 1 and cuts[0] == 0 and cuts[-1] == len(lens)
         assert all(a <= b for a, b in zip(cuts, cuts[1:]))
+
+
+def test_weak_golden_shard(pkg):
+    """bench.py's config-4 weak leg: 65536 chunks per rank cycle through the
+    four golden shards of the 4-way split at any N; sizes that do not divide
+    the list fall back to plain weak shards with no golden index."""
+    import importlib
+    shard = importlib.import_module("congestion-control-with-bittorren_amd.shard")
+    for world in (1, 2, 4, 8):
+        for r in range(world):
+            first, count, k = shard.weak_golden_shard(r, 65536, 262144)
+            assert (first, count) == shard.strong_shard(r % 4, 4, 262144) and k == r % 4
+    assert shard.weak_golden_shard(3, 32768, 262144) == (3 * 32768, 32768, 3)
+    assert shard.weak_golden_shard(9, 32768, 262144) == (32768, 32768, 1)
+    assert shard.weak_golden_shard(2, 100000, 262144) == (200000, 100000, None)

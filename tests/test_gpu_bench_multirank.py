@@ -6,8 +6,9 @@ Weak leg: each rank hashes its own 4096 chunks of config 2 (global ids
 4096 r ..) and checks the digest-of-digests against the reference golden
 aggregate; strong leg: BASELINE config 4's 262144 chunks split in two
 contiguous shards, each checked against the golden shard aggregate of the
-2-way split, plus the whole list on rank 0 against the golden aggregate.
-The JSON line is rank 0's; both parities are ANDed over ranks."""
+2-way split, plus the whole list on rank 0 against the golden aggregate;
+config-4 weak leg: 65536 chunks per rank, rank r checked against the golden
+shard r of the 4-way split.  The JSON line is rank 0's; both parities are ANDed over ranks."""
 import json
 import os
 import socket
@@ -44,3 +45,6 @@ def test_bench_two_ranks_weak_and_strong(pkg):
     assert st["n_gpus"] == 2 and st["chunks_per_gpu"] == 131072 and st["chunks_total"] == 262144
     assert st["parity"] is True and st["one_gpu_parity"] is True
     assert st["speedup"] > 0 and st["efficiency"] == pytest.approx(st["speedup"] / 2, rel=1e-3)
+    w4 = d["weak_config4"]
+    assert w4["n_gpus"] == 2 and w4["chunks_per_gpu"] == 65536 and w4["parity"] is True
+    assert w4["value"] == pytest.approx(2 * 65536 * 524288 / 2**30 / (w4["ms_per_step"] / 1e3), rel=1e-3)
