@@ -1037,6 +1037,40 @@ long hash_file_devices(int fd, off_t pos, off_t end, int nd, int read_threads, F
 }
 }  // namespace
 
+namespace {
+// A regular file of at most SHA1CHUNK_HOST_SMALL bytes (make-chunks on a small
+// file, BASELINE config 1's tmp/C.tar): read and hashed on the host chunk by
+// chunk, as the reference's fread + shahash loop does (chunk.c:15-27), with
+// no pinned slots, streams or code object to set up.  Opt-in like the other
+// small calls; the device must still be present (the caller checked).
+long hash_file_host(int fd, off_t pos, off_t end, FdSink* sk) {
+    std::vector<uint8_t> buf(SHA1CHUNK_CHUNK_LEN);
+    long n = 0;
+    while (pos < end) {
+        const size_t want = static_cast<size_t>(std::min<off_t>(SHA1CHUNK_CHUNK_LEN, end - pos));
+        size_t got = 0;
+        while (got < want) {
+            const ssize_t r = pread(fd, buf.data() + got, want - got, pos + static_cast<off_t>(got));
+            if (r < 0) {
+                if (errno == EINTR) continue;
+                return fail(SHA1CHUNK_EIO, "file read error");
+            }
+            if (r == 0) break;  // the file shrank under us
+            got += static_cast<size_t>(r);
+        }
+        if (got == 0) break;
+        uint8_t dig[20];
+        sha1host_digest(buf.data(), got, dig);
+        fd_sink(sk, static_cast<size_t>(n), dig, 1);
+        ++n;
+        pos += static_cast<off_t>(got);
+        if (got < want) break;
+    }
+    (void)lseek(fd, pos, SEEK_SET);
+    return n;
+}
+}  // namespace
+
 long sha1chunk_hash_fd(int fd, uint8_t* digests, size_t max_chunks, size_t* total_chunks) {
     FdSink sk{digests, max_chunks};
     struct stat st;
@@ -1047,7 +1081,10 @@ long sha1chunk_hash_fd(int fd, uint8_t* digests, size_t max_chunks, size_t* tota
         const int read_threads = e ? std::max(1, atoi(e)) : 8;
         const off_t end = std::max(pos, st.st_size);
         const int nd = file_devices(static_cast<uint64_t>(end - pos));
-        if (nd > 1) {
+        if (host_small_bytes() && static_cast<uint64_t>(end - pos) <= host_small_bytes()) {
+            if (int rc = require_device()) return rc;
+            n = hash_file_host(fd, pos, end, &sk);
+        } else if (nd > 1) {
             n = hash_file_devices(fd, pos, end, nd, read_threads, &sk);
         } else {
             PartPool pool(read_threads - 1);
