@@ -16,9 +16,10 @@
  * SHA1CHUNK_HOST_SMALL=<bytes> in the environment, host calls of at most
  * that many bytes (sha1chunk_hash_batch / verify_batch on host memory,
  * compress_blocks, finish: shahash, get_chunk_hash, verify_hash, the
- * SHA1Update trio) are hashed on the host (x86 SHA extensions) -- one
- * 512 KiB chunk in ~0.2 ms instead of one lane's ~6 ms serial chain -- and
- * the device is still required.
+ * SHA1Update trio; sha1chunk_hash_fd / make_chunks on a regular file of at
+ * most that size; a verify queue of batch 1 whose max length fits) are hashed
+ * on the host (x86 SHA extensions) -- one 512 KiB chunk in ~0.2 ms instead
+ * of one lane's ~6 ms serial chain -- and the device is still required.
  */
 #ifndef SHA1CHUNK_H
 #define SHA1CHUNK_H
