@@ -1,8 +1,10 @@
 """GPU parity: the HIP engine, called through the C ABI, against the oracle
 and the reference's golden vectors.  Bit-exact everywhere (integer work)."""
+import json
 import os
 import subprocess
 import sys
+import time
 
 import numpy as np
 import pytest
@@ -265,6 +267,39 @@ def test_reference_make_chunks_main_dropin(pkg, dev, golden, fixture_files, tmp_
         r = subprocess.run([exe, str(p)], capture_output=True, text=True, timeout=60)
         assert r.returncode == 0, r.stderr
         assert r.stdout == "".join(f"{i} {h}\n" for i, h in enumerate(want)), name
+
+
+def test_config1_make_chunks_cli(pkg, dev, golden, fixture_files, tmp_path):
+    """BASELINE config 1 (make-chunks on tmp/C.tar, 4 chunks), every way the
+    CLI can run here, each against tmp/C.chunks: the reference's own
+    make-chunks built from its sources (oracle/_ref, CPU sha.c), the repo's
+    CLI (device, and the host small-file path with SHA1CHUNK_HOST_SMALL at
+    4 MiB), and the reference main linked against the library with the knob.
+    Prints the median wall time of 5 runs of each (process start included)."""
+    p = tmp_path / "C.tar"
+    p.write_bytes(fixture_files["tmp/C.tar"])
+    want = "".join(f"{i} {h}\n" for i, h in enumerate(golden["fixtures"]["C.chunks_file"]))
+    runs = {"repo_cli_device": (os.path.join(PKG_DIR, "make-chunks"), {}),
+            "repo_cli_host_small": (os.path.join(PKG_DIR, "make-chunks"), {"SHA1CHUNK_HOST_SMALL": "4194304"})}
+    ref_exe = os.path.join(ROOT, "oracle", "_ref", "make-chunks")
+    dropin = os.path.join(ROOT, "oracle", "_ref", "dropin", "make-chunks")
+    if os.path.exists(ref_exe):
+        runs["reference_sha_c"] = (ref_exe, {})
+    if os.path.exists(dropin):
+        runs["reference_main_dropin_host_small"] = (dropin, {"SHA1CHUNK_HOST_SMALL": "4194304"})
+    times = {}
+    for name, (exe, extra) in runs.items():
+        env = dict(os.environ, **extra)
+        ts = []
+        for _ in range(5):
+            t0 = time.perf_counter()
+            r = subprocess.run([exe, str(p)], capture_output=True, text=True, env=env, timeout=60)
+            ts.append(time.perf_counter() - t0)
+            assert r.returncode == 0, (name, r.stderr)
+            # the reference prints CRLF-free "%d %s\n" lines (make_chunks.c:53)
+            assert r.stdout.replace("\r\n", "\n") == want, (name, r.stdout)
+        times[name] = round(sorted(ts)[2] * 1e3, 2)
+    print("config1_cli_ms " + json.dumps(times))
 
 
 def test_reference_receive_path_dropin(pkg, dev, golden, fixture_files, tmp_path):

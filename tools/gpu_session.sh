@@ -35,6 +35,8 @@ for s in $STEPS; do
     test)  run pytest_gpu 900 python -u -m pytest tests -v -m gpu -p no:cacheprovider --timeout 300 --timeout-method thread ;;
     fuzz)  SHA1CHUNK_FUZZ_SEEDS=600 run fuzz 600 python -u -m pytest tests/test_gpu_fuzz.py \
                tests/test_gpu_vq_persistent.py -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+    cfg1)  run cfg1 300 python -u -m pytest tests/test_gpu_parity.py -m gpu -s -q -p no:cacheprovider \
+               -k test_config1_make_chunks_cli --timeout 200 --timeout-method thread ;;
     smoke) run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     sweep) run sweep 600 python tools/sweep.py --chunks 1024,4096,16384,65536,131072 --rounds 2 --out "$OUT/sweep.json" ;;
     bench) run bench 600 python bench.py --steps 10 --warmup 2 ;;
