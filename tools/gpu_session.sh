@@ -67,6 +67,8 @@ for s in $STEPS; do
                  --out "$OUT/shardprod.json" ;;
     rehearse2) SHA1_BENCH_DIST_BACKEND=gloo run rehearse2 600 python -m torch.distributed.run --nnodes=1 \
                    --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 2 ;;
+    rehearse4) SHA1_BENCH_DIST_BACKEND=gloo run rehearse4 600 python -m torch.distributed.run --nnodes=1 \
+                   --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 4 --steps 10 --warmup 2 ;;
     vqbench) run vqbench 600 python tools/vq_bench.py --chunks 16384 --batches 64,256,1024 --reps 3 \
                  --out "$OUT/vq_bench.json" ;;
     vqhost1) run vqhost1 300 python tools/vq_bench.py --chunks 4096 --batches 64 --reps 2 \
