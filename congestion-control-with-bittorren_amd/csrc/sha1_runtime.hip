@@ -267,9 +267,73 @@ int get_device(Device** out) {
 
 // The library's contract for every call, host small-call path included: a
 // gfx950 device is present and the thread's device index is valid.
+// Presence check of the host small-call paths, without starting the HIP
+// runtime (50-250 ms in a fresh process, profiles/startup_r03.json; the
+// whole of make-chunks on a small file otherwise): the kernel driver's KFD
+// topology lists gfx950 agents (gfx_target_version 90500) whose render node
+// this process may open, next to an accessible /dev/kfd, and no GPU agent of
+// another kind -- probe()'s rule that every device be gfx950.  Returns the
+// agent count, 0 when none is visible, or -1 when it cannot tell (a
+// *_VISIBLE_DEVICES mask is set, or the topology is unreadable): then the
+// HIP probe decides.
+std::string g_light_err;
+int light_count() {
+    static std::once_flag once;
+    static int count = -1;
+    std::call_once(once, [] {
+        for (const char* v : {"HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
+                              "GPU_DEVICE_ORDINAL"})
+            if (getenv(v)) return;
+        if (access("/dev/kfd", R_OK | W_OK) != 0) {
+            count = 0;
+            g_light_err = "no HIP device visible (/dev/kfd not accessible)";
+            return;
+        }
+        const char* dir = "/sys/class/kfd/kfd/topology/nodes";
+        int n = 0;
+        for (int node = 0; node < 1024; ++node) {
+            char path[128];
+            snprintf(path, sizeof path, "%s/%d/properties", dir, node);
+            FILE* f = fopen(path, "r");
+            if (!f) {
+                if (node == 0) return;  // no topology to read
+                break;
+            }
+            char key[64];
+            unsigned long long val;
+            unsigned long long target = 0, minor = 0;
+            while (fscanf(f, "%63s %llu", key, &val) == 2) {
+                if (!strcmp(key, "gfx_target_version")) target = val;
+                if (!strcmp(key, "drm_render_minor")) minor = val;
+            }
+            fclose(f);
+            if (target == 0) continue;  // a CPU agent
+            if (target != 90500) {
+                count = 0;
+                g_light_err = "a GPU agent is gfx_target_version " + std::to_string(target) +
+                              ", this build targets gfx950 only";
+                return;
+            }
+            snprintf(path, sizeof path, "/dev/dri/renderD%llu", minor);
+            if (access(path, R_OK | W_OK) == 0) ++n;
+        }
+        count = n;
+        if (n == 0) g_light_err = "no HIP device visible (no accessible gfx950 agent)";
+    });
+    return count;
+}
+
 int require_device() {
-    if (device_count() <= 0) return fail(SHA1CHUNK_ENODEV, "%s", g_probe_err.c_str());
-    if (t_dev < 0 || t_dev >= g_count) return fail(SHA1CHUNK_EINVAL, "bad device %d", t_dev);
+    const int lc = light_count();
+    if (lc < 0) {
+        if (device_count() <= 0) return fail(SHA1CHUNK_ENODEV, "%s", g_probe_err.c_str());
+        if (t_dev < 0 || t_dev >= g_count) return fail(SHA1CHUNK_EINVAL, "bad device %d", t_dev);
+        return SHA1CHUNK_OK;
+    }
+    if (lc == 0) return fail(SHA1CHUNK_ENODEV, "%s", g_light_err.c_str());
+    int k = lc;  // logical devices, as probe() counts them
+    if (const char* e = getenv("SHA1CHUNK_VIRTUAL_DEVICES")) k = std::max(1, std::min(64, atoi(e)));
+    if (t_dev < 0 || t_dev >= k) return fail(SHA1CHUNK_EINVAL, "bad device %d", t_dev);
     return SHA1CHUNK_OK;
 }
 
@@ -983,8 +1047,9 @@ namespace {
 // chunk list split per device, SURVEY.md 8e: no collective).
 int file_devices(uint64_t bytes) {
     const char* e = getenv("SHA1CHUNK_FILE_DEVICES");
+    if (!e) return 1;
     const int nd = device_count();
-    if (!e || nd <= 1) return 1;
+    if (nd <= 1) return 1;
     const int want = strcmp(e, "all") == 0 ? nd : std::max(1, std::min(nd, atoi(e)));
     // at least one chunk per device
     const uint64_t chunks = (bytes + SHA1CHUNK_CHUNK_LEN - 1) / SHA1CHUNK_CHUNK_LEN;
@@ -1080,8 +1145,9 @@ long sha1chunk_hash_fd(int fd, uint8_t* digests, size_t max_chunks, size_t* tota
         const char* e = getenv("SHA1CHUNK_READ_THREADS");
         const int read_threads = e ? std::max(1, atoi(e)) : 8;
         const off_t end = std::max(pos, st.st_size);
-        const int nd = file_devices(static_cast<uint64_t>(end - pos));
-        if (host_small_bytes() && static_cast<uint64_t>(end - pos) <= host_small_bytes()) {
+        const bool host = host_small_bytes() && static_cast<uint64_t>(end - pos) <= host_small_bytes();
+        const int nd = host ? 1 : file_devices(static_cast<uint64_t>(end - pos));
+        if (host) {
             if (int rc = require_device()) return rc;
             n = hash_file_host(fd, pos, end, &sk);
         } else if (nd > 1) {
