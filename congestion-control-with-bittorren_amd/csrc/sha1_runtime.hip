@@ -270,35 +270,49 @@ int get_device(Device** out) {
 // Presence check of the host small-call paths, without starting the HIP
 // runtime (50-250 ms in a fresh process, profiles/startup_r03.json; the
 // whole of make-chunks on a small file otherwise): the kernel driver's KFD
-// topology lists gfx950 agents (gfx_target_version 90500) whose render node
-// this process may open, next to an accessible /dev/kfd, and no GPU agent of
-// another kind -- probe()'s rule that every device be gfx950.  Returns the
-// agent count, 0 when none is visible, or -1 when it cannot tell (a
-// *_VISIBLE_DEVICES mask is set, or the topology is unreadable): then the
-// HIP probe decides.
+// topology lists gfx950 agents (gfx_target_version 90500) whose properties
+// and render node this process may open, next to an accessible /dev/kfd,
+// and no such GPU agent of another kind -- probe()'s rule that every device
+// be gfx950.  Agents this process cannot read (a container that exposes one
+// GPU of a node) are not its devices.  A *_VISIBLE_DEVICES mask caps the
+// count at its number of entries.  Returns the device count, 0 when none is
+// visible, or -1 when it cannot tell (no readable topology, an empty mask):
+// then the HIP probe decides.
 std::string g_light_err;
 int light_count() {
     static std::once_flag once;
     static int count = -1;
     std::call_once(once, [] {
-        for (const char* v : {"HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
-                              "GPU_DEVICE_ORDINAL"})
-            if (getenv(v)) return;
+        int masked = 1 << 30;
+        for (const char* v : {"ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
+                              "GPU_DEVICE_ORDINAL"}) {
+            const char* m = getenv(v);
+            if (!m) continue;
+            int tokens = 0;
+            for (const char* c = m; *c;) {
+                const char* e = strchr(c, ',');
+                const size_t len = e ? static_cast<size_t>(e - c) : strlen(c);
+                if (len) ++tokens;
+                c += len + (e ? 1 : 0);
+            }
+            if (tokens == 0) return;
+            masked = std::min(masked, tokens);
+        }
         if (access("/dev/kfd", R_OK | W_OK) != 0) {
             count = 0;
             g_light_err = "no HIP device visible (/dev/kfd not accessible)";
             return;
         }
         const char* dir = "/sys/class/kfd/kfd/topology/nodes";
-        int n = 0;
-        for (int node = 0; node < 1024; ++node) {
+        int n = 0, readable = 0;
+        for (int node = 0; node < 4096; ++node) {
             char path[128];
+            snprintf(path, sizeof path, "%s/%d", dir, node);
+            if (access(path, F_OK) != 0) break;
             snprintf(path, sizeof path, "%s/%d/properties", dir, node);
             FILE* f = fopen(path, "r");
-            if (!f) {
-                if (node == 0) return;  // no topology to read
-                break;
-            }
+            if (!f) continue;  // not this process's agent
+            ++readable;
             char key[64];
             unsigned long long val;
             unsigned long long target = 0, minor = 0;
@@ -308,17 +322,19 @@ int light_count() {
             }
             fclose(f);
             if (target == 0) continue;  // a CPU agent
+            snprintf(path, sizeof path, "/dev/dri/renderD%llu", minor);
+            if (access(path, R_OK | W_OK) != 0) continue;
             if (target != 90500) {
                 count = 0;
                 g_light_err = "a GPU agent is gfx_target_version " + std::to_string(target) +
                               ", this build targets gfx950 only";
                 return;
             }
-            snprintf(path, sizeof path, "/dev/dri/renderD%llu", minor);
-            if (access(path, R_OK | W_OK) == 0) ++n;
+            ++n;
         }
-        count = n;
-        if (n == 0) g_light_err = "no HIP device visible (no accessible gfx950 agent)";
+        if (readable == 0) return;
+        count = std::min(n, masked);
+        if (count == 0) g_light_err = "no HIP device visible (no accessible gfx950 agent)";
     });
     return count;
 }
