@@ -152,7 +152,11 @@ def main():
     # SHA1_BENCH_DIST_BACKEND=gloo rehearses several ranks on one GPU.
     backend = os.environ.get("SHA1_BENCH_DIST_BACKEND", "nccl")
     cdev = "cuda" if backend == "nccl" else "cpu"
-    if world > 1:
+    # SHA1_BENCH_FORCE_PG=1 (under torchrun): a process group even at N = 1,
+    # so a one-GPU box runs the RCCL control plane (init with device_id,
+    # barrier, all_reduce MAX/MIN) that an 8-GPU node runs
+    use_pg = world > 1 or os.environ.get("SHA1_BENCH_FORCE_PG") == "1"
+    if use_pg:
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
         else:
@@ -187,7 +191,7 @@ def main():
 
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(a.steps)]
-    if world > 1:
+    if use_pg:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -195,7 +199,7 @@ def main():
         step(i, e0, e1)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    if world > 1:
+    if use_pg:
         dist.barrier()
     kern_ms = float(np.mean([e0.elapsed_time(e1) for e0, e1 in evs]))
     elapsed, kern_ms = shard.max_over_ranks([t1 - t0, kern_ms], device=cdev)
@@ -315,9 +319,11 @@ def main():
         if "latency_one_chunk" in result:
             result["latency_one_chunk"]["reference_sha_c_one_core_ms"] = \
                 result["cpu_baseline"].pop("one_chunk_ms")
+    if use_pg:
+        result["config"]["control_plane"] = f"torch.distributed {backend}, world {world}"
     if rank == 0:
         print(json.dumps(result), flush=True)
-    if world > 1:
+    if use_pg:
         dist.destroy_process_group()
 
 

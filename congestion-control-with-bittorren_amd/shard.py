@@ -83,10 +83,11 @@ def byte_balanced_cuts(lengths, world: int) -> list[int]:
 
 
 def max_over_ranks(values, device=None) -> list[float]:
-    """Element-wise max over ranks (identity without an initialised group)."""
+    """Element-wise max over ranks (identity without an initialised group;
+    with one, the all_reduce runs even at world size 1)."""
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return [float(v) for v in values]
     t = torch.tensor([float(v) for v in values], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -96,7 +97,7 @@ def max_over_ranks(values, device=None) -> list[float]:
 def all_ranks_ok(flag: bool, device=None) -> bool:
     import torch
     import torch.distributed as dist
-    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+    if not (dist.is_available() and dist.is_initialized()):
         return bool(flag)
     t = torch.tensor([1.0 if flag else 0.0], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MIN)

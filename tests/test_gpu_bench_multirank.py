@@ -48,3 +48,24 @@ def test_bench_two_ranks_weak_and_strong(pkg):
     w4 = d["weak_config4"]
     assert w4["n_gpus"] == 2 and w4["chunks_per_gpu"] == 65536 and w4["parity"] is True
     assert w4["value"] == pytest.approx(2 * 65536 * 524288 / 2**30 / (w4["ms_per_step"] / 1e3), rel=1e-3)
+
+
+def test_bench_rccl_control_plane_one_rank(pkg):
+    """The RCCL control plane bench.py uses on an 8-GPU node (process group
+    over "nccl" = RCCL with device_id, barrier, all_reduce MAX of the times,
+    all_reduce MIN of the parity flags), run at world size 1 on the test box
+    (SHA1_BENCH_FORCE_PG=1 under torch.distributed.run): same JSON line,
+    parity on every leg."""
+    env = dict(os.environ, SHA1_BENCH_FORCE_PG="1")
+    env.pop("SHA1_BENCH_DIST_BACKEND", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "1",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+           "--steps", "3", "--warmup", "1", "--strong-steps", "1", "--no-latency", "--no-cpu-baseline"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["config"]["control_plane"] == "torch.distributed nccl, world 1"
+    assert d["n_gpus"] == 1 and d["parity"] is True and d["value"] > 0
+    assert d["strong"]["parity"] is True and d["weak_config4"]["parity"] is True
