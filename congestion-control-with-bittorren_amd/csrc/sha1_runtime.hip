@@ -265,8 +265,6 @@ int get_device(Device** out) {
     return SHA1CHUNK_OK;
 }
 
-// The library's contract for every call, host small-call path included: a
-// gfx950 device is present and the thread's device index is valid.
 // Presence check of the host small-call paths, without starting the HIP
 // runtime (50-250 ms in a fresh process, profiles/startup_r03.json; the
 // whole of make-chunks on a small file otherwise): the kernel driver's KFD
@@ -339,6 +337,8 @@ int light_count() {
     return count;
 }
 
+// The library's contract for every call, host small-call path included: a
+// gfx950 device is present and the thread's device index is valid.
 int require_device() {
     const int lc = light_count();
     if (lc < 0) {
