@@ -1605,8 +1605,32 @@ int pvq_wait(Pvq* P, Pred pred, const char* what) {
     }
 }
 
+// Queues alive at process exit (a caller that never destroys its queue):
+// an exit handler raises every live drain's stop word and waits for its
+// launches, so no drain wave is still polling the pinned ring when the
+// runtime and the process's mappings go away.  The handler is registered at
+// the first queue, after HIP's own start-up, so it runs before HIP's
+// teardown (exit handlers run in reverse order).
+std::mutex g_pvq_mu;
+std::vector<Pvq*>* g_pvq_live = nullptr;
+void pvq_stop_all_at_exit();
+void pvq_track(Pvq* P, bool add) {
+    std::lock_guard<std::mutex> lk(g_pvq_mu);
+    if (!g_pvq_live) {
+        if (!add) return;
+        g_pvq_live = new std::vector<Pvq*>();
+        std::atexit(pvq_stop_all_at_exit);
+    }
+    auto& v = *g_pvq_live;
+    if (add)
+        v.push_back(P);
+    else
+        v.erase(std::remove(v.begin(), v.end(), P), v.end());
+}
+
 void pvq_destroy(Pvq* P) {
     if (!P) return;
+    pvq_track(P, false);
     (void)hipSetDevice(P->dev);
     if (P->ctl) {
         __atomic_store_n(&P->ctl->stop, 1u, __ATOMIC_RELEASE);
@@ -1676,7 +1700,21 @@ Pvq* pvq_create(Device* D, size_t batch, uint32_t max_chunk_len) {
             return nullptr;
         }
     P->copier = new PartPool(vq_copy_helpers());
+    pvq_track(P, true);
     return P;
+}
+
+void pvq_stop_all_at_exit() {
+    std::lock_guard<std::mutex> lk(g_pvq_mu);
+    if (!g_pvq_live) return;
+    for (Pvq* P : *g_pvq_live)
+        if (P->ctl) __atomic_store_n(&P->ctl->stop, 1u, __ATOMIC_RELEASE);
+    __atomic_thread_fence(__ATOMIC_SEQ_CST);
+    for (Pvq* P : *g_pvq_live) {
+        (void)hipSetDevice(P->dev);
+        for (int k = 0; k < 2; ++k)
+            if (P->stream[k]) (void)hipStreamSynchronize(P->stream[k]);
+    }
 }
 
 int pvq_submit(Pvq* P, const void* chunk, uint32_t len, const uint8_t expected[20], uint64_t tag) {

@@ -205,3 +205,35 @@ def test_device_batches_run_beside_a_busy_drain(pkg, dev, persistent):
     assert got == {t: 0 for t in range(1024)}
     assert np.array_equal(dig.cpu().numpy(), want)
     assert dev_s < 5.0
+
+
+def test_process_exit_with_a_live_drain(pkg):
+    """A caller that exits while its queue's drain is busy and never destroys
+    the queue (a C program returning from main): the library's exit handler
+    raises the stop word and waits for the drain, so the process ends cleanly
+    (exit status 0, within seconds) instead of tearing down the pinned ring
+    under running waves.  Idle exit set high (10 s) so the drain is surely
+    alive at exit."""
+    import subprocess
+    import sys
+    code = (
+        "import ctypes, hashlib, os, sys\n"
+        "lib = ctypes.CDLL(sys.argv[1])\n"
+        "lib.sha1chunk_vq_create.restype = ctypes.c_void_p\n"
+        "lib.sha1chunk_vq_submit.argtypes = [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_uint32,\n"
+        "                                    ctypes.c_char_p, ctypes.c_uint64]\n"
+        "q = lib.sha1chunk_vq_create(ctypes.c_size_t(64), ctypes.c_uint32(524288))\n"
+        "assert q\n"
+        "data = os.urandom(524288); d = hashlib.sha1(data).digest()\n"
+        "for t in range(256):\n"
+        "    assert lib.sha1chunk_vq_submit(q, data, 524288, d, t) == 0\n"
+        "print('submitted', flush=True)\n")
+    env = dict(os.environ, SHA1CHUNK_VQ_MODE="persistent", SHA1CHUNK_VQ_IDLE_MS="10000")
+    libp = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                        "congestion-control-with-bittorren_amd", "libsha1chunk.so")
+    t0 = time.time()
+    r = subprocess.run([sys.executable, "-c", code, libp], capture_output=True, text=True, env=env,
+                       timeout=90)
+    secs = time.time() - t0
+    assert r.returncode == 0 and "submitted" in r.stdout, (r.stdout, r.stderr[-2000:])
+    assert secs < 60, secs
