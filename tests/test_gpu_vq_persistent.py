@@ -236,4 +236,4 @@ def test_process_exit_with_a_live_drain(pkg):
                        timeout=90)
     secs = time.time() - t0
     assert r.returncode == 0 and "submitted" in r.stdout, (r.stdout, r.stderr[-2000:])
-    assert secs < 60, secs
+    assert secs < 8, secs  # not the 10 s idle exit: the stop word ended the drain
