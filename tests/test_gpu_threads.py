@@ -9,7 +9,8 @@ the SHA1Init/Update/Final trio at random split points, ragged host batches,
 verify_batch, make_chunks on a file, and a verify queue of their own -- and
 every digest is checked against hashlib.  The same run again in a child
 process with SHA1CHUNK_HOST_SMALL=524288 mixes the host small-call path with
-the device paths under the same concurrency."""
+the device paths under the same concurrency, and with the threads bound to
+three logical devices."""
 import os
 import subprocess
 import sys
@@ -33,6 +34,8 @@ tmp = tempfile.mkdtemp()
 
 def work(tid):
     rng = np.random.default_rng(1000 + tid)
+    if os.environ.get("SHA1CHUNK_VIRTUAL_DEVICES"):  # threads spread over the logical devices
+        pkg.set_device(tid % pkg.device_count())
     ops = 0
     with pkg.VerifyQueue(batch=8, max_chunk_len=L) as q:
         want_q = {}
@@ -114,3 +117,10 @@ def test_concurrent_callers(pkg, mode):
 
 def test_concurrent_callers_host_small(pkg):
     _run({"SHA1CHUNK_HOST_SMALL": "524288"})
+
+
+def test_concurrent_callers_over_devices(pkg):
+    """Threads bound to different devices (three logical devices over the
+    box's GPU, SHA1CHUNK_VIRTUAL_DEVICES=3, each with its own streams, slots
+    and queues)."""
+    _run({"SHA1CHUNK_VIRTUAL_DEVICES": "3"})
