@@ -1334,7 +1334,7 @@ struct sha1chunk_vq {
 
 namespace {
 
-uint64_t* vq_off(sha1chunk_vq* q, uint8_t* base) { return reinterpret_cast<uint64_t*>(base); }
+uint64_t* vq_off(sha1chunk_vq*, uint8_t* base) { return reinterpret_cast<uint64_t*>(base); }  // offsets lead the set
 uint32_t* vq_len(sha1chunk_vq* q, uint8_t* base) {
     return reinterpret_cast<uint32_t*>(base + q->cap * 8);
 }
