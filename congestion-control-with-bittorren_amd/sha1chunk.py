@@ -378,6 +378,30 @@ def synth_fill_ragged_device(base, offsets, lengths, first: int, seed: int = SEE
            "sha1chunk_synth_fill_ragged_async")
 
 
+def _splitmix64(x: np.ndarray) -> np.ndarray:
+    with np.errstate(over="ignore"):
+        z = x + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def mixed_lengths(n: int, seed: int = SEED) -> np.ndarray:
+    """Chunk lengths of the synthetic mixed batch (BASELINE config 5, the
+    received-chunk verify shape): chunk i draws an
+    octave o in 0..7 and a mantissa m in 0..4095 from splitmix64 and is
+    (4096 + m) << o bytes (4 KiB .. just under 1 MiB); every 7th chunk gets
+    1..63 more bytes so its tail is not 64-byte aligned.  The golden digests
+    of tests/golden/ were generated over these lengths by the reference."""
+    i = np.arange(n, dtype=np.uint64)
+    r = _splitmix64(np.uint64(seed + 1) ^ i)
+    octave = (r & np.uint64(7)).astype(np.uint32)
+    mant = ((r >> np.uint64(8)) & np.uint64(4095)).astype(np.uint32)
+    ln = (np.uint32(4096) + mant) << octave
+    tail = (_splitmix64(np.uint64(seed + 2) ^ i) % np.uint64(63)).astype(np.uint32) + 1
+    return np.where(i % 7 == 6, ln + tail, ln).astype(np.uint32)
+
+
 def ragged_layout(lengths: Iterable[int], align: int = 128) -> tuple[np.ndarray, int]:
     """Offsets packing chunks back to back at `align`-byte boundaries."""
     ln = np.asarray(list(lengths) if not isinstance(lengths, np.ndarray) else lengths, np.uint64)

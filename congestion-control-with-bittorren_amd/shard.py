@@ -82,6 +82,65 @@ def byte_balanced_cuts(lengths, world: int) -> list[int]:
     return cuts
 
 
+class DeviceMapError(RuntimeError):
+    """A multi-rank run would put two ranks on one GPU (or a rank on none)."""
+
+
+def device_for_local_rank(local_rank: int, local_world: int, device_count: int,
+                          shared_ok: bool = False) -> int:
+    """The GPU of local rank `local_rank`: one process per GPU, rank r on
+    device r.  A node that exposes fewer devices than it runs local ranks
+    would stack ranks onto shared GPUs and time a plausible but wrong curve,
+    so that raises -- unless `shared_ok` (the gloo rehearsal of several ranks
+    on one card, SHA1_BENCH_DIST_BACKEND=gloo), which maps round robin."""
+    if device_count <= 0:
+        raise DeviceMapError("no GPU visible to this rank")
+    if local_world > device_count and not shared_ok:
+        raise DeviceMapError(
+            f"{local_world} local ranks but only {device_count} visible GPU(s): one rank per GPU "
+            "is required (set HIP_VISIBLE_DEVICES / --nproc-per-node to match)")
+    if local_rank < 0 or (local_rank >= device_count and not shared_ok):
+        raise DeviceMapError(f"local rank {local_rank} has no GPU of its own ({device_count} visible)")
+    return local_rank % device_count
+
+
+def device_identity(host: str, rank: int, local_rank: int, ordinal: int, props) -> dict:
+    """What a rank records about its GPU (bench.py gathers these on rank 0):
+    the ordinal and the physical identity (PCI domain:bus:device and UUID)."""
+    pci = None
+    if props is not None and hasattr(props, "pci_bus_id"):
+        pci = "%04x:%02x:%02x" % (getattr(props, "pci_domain_id", 0), props.pci_bus_id,
+                                  getattr(props, "pci_device_id", 0))
+    uuid = str(getattr(props, "uuid", "")) if props is not None else ""
+    return {"rank": rank, "host": host, "local_rank": local_rank, "device": ordinal,
+            "pci": pci, "uuid": uuid}
+
+
+def check_distinct_devices(identities: list[dict], shared_ok: bool = False) -> None:
+    """Raise when two ranks on one host share a physical GPU (same UUID, or
+    same PCI address where no UUID is reported)."""
+    if shared_ok:
+        return
+    seen: dict = {}
+    for ident in identities:
+        phys = ident.get("uuid") or ident.get("pci") or f"ordinal {ident.get('device')}"
+        key = (ident.get("host"), phys)
+        if key in seen:
+            raise DeviceMapError(f"ranks {seen[key]} and {ident.get('rank')} share GPU {phys} on "
+                                 f"{ident.get('host')}: a scaling run needs one GPU per rank")
+        seen[key] = ident.get("rank")
+
+
+def gather_identities(ident: dict) -> list[dict]:
+    """Every rank's identity, in rank order (just this one without a group)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        return [ident]
+    out: list = [None] * dist.get_world_size()
+    dist.all_gather_object(out, ident)
+    return out
+
+
 def max_over_ranks(values, device=None) -> list[float]:
     """Element-wise max over ranks (identity without an initialised group;
     with one, the all_reduce runs even at world size 1)."""

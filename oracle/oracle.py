@@ -41,6 +41,9 @@ def _declare(lib: C.CDLL, prefix: str) -> C.CDLL:
     getattr(lib, prefix + "time_synth").argtypes = [C.c_uint64, C.c_uint64, C.c_uint32,
                                                     C.c_uint64, C.c_int, _u8p]
     getattr(lib, prefix + "time_synth").restype = C.c_double
+    if prefix == "ref_":
+        lib.ref_time_batch.argtypes = [_u8p, _u64p, _u32p, C.c_size_t, _u8p, C.c_int]
+        lib.ref_time_batch.restype = C.c_double
     return lib
 
 
@@ -124,6 +127,22 @@ def splitmix64(x: int) -> int:
 
 def digest_of_digests(digests: np.ndarray) -> bytes:
     return shahash(np.ascontiguousarray(digests, dtype=np.uint8).tobytes())
+
+
+def time_batch(base: np.ndarray, offsets: np.ndarray, lengths: np.ndarray, threads: int = 1,
+               opt: str = "O2") -> tuple[float, np.ndarray]:
+    """Seconds for the reference sha.c (oracle/_ref, -O2 or its own Makefile
+    flags "O0") to hash a batch already in memory, and its digests."""
+    r = ref_lib(opt)
+    if r is None:
+        raise FileNotFoundError(f"oracle/_ref reference build {opt} missing")
+    base = np.ascontiguousarray(base, dtype=np.uint8)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+    out = np.zeros((len(off), 20), np.uint8)
+    secs = r.ref_time_batch(_p(base, _u8p), _p(off, _u64p), _p(ln, _u32p), len(off), _p(out, _u8p),
+                            threads)
+    return float(secs), out
 
 
 def time_synth(count: int, chunk_len: int = CHUNK_LEN, threads: int = 1, first: int = 0,

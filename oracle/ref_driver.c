@@ -80,3 +80,15 @@ double ref_time_synth(uint64_t first, uint64_t count, uint32_t chunk_len, uint64
     free(buf); free(off); free(len); free(dig);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* Seconds to hash n chunks already in memory with the reference sha.c on
+ * `threads` pthreads (chunk-strided), digests into dig: the CPU-baseline
+ * rows of bench.py time the same bytes on every build and thread count. */
+double ref_time_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, size_t n,
+                      uint8_t *dig, int threads) {
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    ref_hash_batch(base, off, len, n, dig, threads);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

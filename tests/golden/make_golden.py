@@ -16,6 +16,10 @@ Outputs (small; committed):
   synth_4096x512k.bin     all 4096 digests of BASELINE config 2
   mixed_16384.bin         all digests of BASELINE config 5 (mixed lengths)
   mixed_16384_len.bin     its 16384 chunk lengths (uint32 LE)
+
+`python tests/golden/make_golden.py --add config5x4` adds only the 4x config-5
+aggregate (65536 chunks of the same length law, bench.py's config5 leg) to an
+existing golden.json.
 """
 from __future__ import annotations
 
@@ -76,7 +80,52 @@ def synth_digests(first: int, count: int, chunk_len: int, slice_chunks: int = 10
     return out
 
 
+def mixed_golden(n: int) -> dict:
+    """Digests of n chunks of the config-5 length law (chunk i: length
+    mixed_len(i), content synth_chunk(i, len)), hashed by the reference in
+    slices so host memory stays bounded: aggregate, lengths hash and a sample."""
+    ln = O.mixed_lengths(n)
+    dig = np.zeros((n, 20), np.uint8)
+    step = 4096
+    for i0 in range(0, n, step):
+        part = ln[i0:i0 + step]
+        off = np.zeros(part.size, np.uint64)
+        pad = (part.astype(np.uint64) + 127) // 128 * 128
+        off[1:] = np.cumsum(pad)[:-1]
+        buf = np.zeros(int(pad.sum()), np.uint8)
+        for j in range(part.size):
+            L = int(part[j])
+            buf[int(off[j]):int(off[j]) + L] = O.synth_chunk(i0 + j, L)
+        dig[i0:i0 + part.size] = ref_digests(buf, off, part)
+    longest = int(np.argmax(ln))
+    sample = sorted(set(list(range(0, n, 997)) + [n - 1, longest]))
+    return {"chunks": n, "total_bytes": int(ln.astype(np.uint64).sum()),
+            "agg": O.digest_of_digests(dig).hex(),
+            "lengths_sha1": hashlib.sha1(ln.tobytes()).hexdigest(),
+            "sample": {str(i): dig[i].tobytes().hex() for i in sample}}
+
+
+def add_config5x4() -> None:
+    O.build(ref=True)
+    assert O.ref_lib() is not None, "reference build failed"
+    path = os.path.join(OUT, "golden.json")
+    g = json.load(open(path))
+    t0 = time.time()
+    g["config5x4"] = mixed_golden(4 * 16384)
+    # its first 16384 chunks are config 5 itself
+    d5 = np.fromfile(os.path.join(OUT, "mixed_16384.bin"), np.uint8).reshape(-1, 20)
+    for k, v in g["config5x4"]["sample"].items():
+        if int(k) < 16384:
+            assert d5[int(k)].tobytes().hex() == v, k
+    print(f"config5x4 {time.time() - t0:.1f}s", flush=True)
+    with open(path, "w") as f:
+        json.dump(g, f, indent=1, sort_keys=True)
+    print("wrote", path)
+
+
 def main() -> None:
+    if sys.argv[1:] == ["--add", "config5x4"]:
+        return add_config5x4()
     O.build(ref=True)
     assert O.ref_lib() is not None, "reference build failed"
     g: dict = {"seed": O.SEED, "chunk_len": O.CHUNK_LEN,

@@ -141,3 +141,73 @@ def test_weak_golden_shard(pkg):
     assert shard.weak_golden_shard(3, 32768, 262144) == (3 * 32768, 32768, 3)
     assert shard.weak_golden_shard(9, 32768, 262144) == (32768, 32768, 1)
     assert shard.weak_golden_shard(2, 100000, 262144) == (200000, 100000, None)
+
+
+def test_device_map_one_rank_per_gpu():
+    """bench.py's device rule: rank r on GPU r, and a
+    node exposing fewer GPUs than local ranks fails instead of stacking
+    ranks on shared devices (the gloo rehearsal may share, round robin)."""
+    import importlib
+    shard = importlib.import_module("congestion-control-with-bittorren_amd.shard")
+    assert [shard.device_for_local_rank(r, 8, 8) for r in range(8)] == list(range(8))
+    with pytest.raises(shard.DeviceMapError, match="only 1 visible"):
+        shard.device_for_local_rank(1, 2, 1)
+    with pytest.raises(shard.DeviceMapError, match="no GPU"):
+        shard.device_for_local_rank(0, 1, 0)
+    assert [shard.device_for_local_rank(r, 4, 1, shared_ok=True) for r in range(4)] == [0, 0, 0, 0]
+    idents = [shard.device_identity("h", r, r, r, None) for r in range(2)]
+    idents[0]["uuid"], idents[1]["uuid"] = "GPU-a", "GPU-b"
+    shard.check_distinct_devices(idents)
+    idents[1]["uuid"] = "GPU-a"
+    with pytest.raises(shard.DeviceMapError, match="share GPU"):
+        shard.check_distinct_devices(idents)
+    shard.check_distinct_devices(idents, shared_ok=True)
+    idents[1]["host"] = "other"  # same UUID string on another host is another card
+    shard.check_distinct_devices(idents)
+
+
+def _ident_worker(rank, world, port, out_dir, same):
+    import importlib
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    shard = importlib.import_module("congestion-control-with-bittorren_amd.shard")
+    ident = shard.device_identity("node0", rank, rank, 0 if same else rank, None)
+    ident["uuid"] = "GPU-0" if same else f"GPU-{rank}"
+    idents = shard.gather_identities(ident)
+    try:
+        shard.check_distinct_devices(idents)
+        verdict = 1.0
+    except shard.DeviceMapError:
+        verdict = 0.0
+    np.save(os.path.join(out_dir, f"i{rank}.npy"),
+            np.array([verdict, len(idents), idents[1]["rank"]], dtype=np.float64))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("same", [False, True])
+def test_two_rank_device_identity_gather(tmp_path, same):
+    """Every rank gathers every rank's GPU identity and reaches the same
+    verdict: two ranks on one physical GPU fail on both ranks."""
+    mp.start_processes(_ident_worker, args=(2, _free_port(), str(tmp_path), same), nprocs=2,
+                       join=True, start_method="spawn")
+    for r in range(2):
+        v = np.load(tmp_path / f"i{r}.npy")
+        assert v[0] == (0.0 if same else 1.0) and v[1] == 2 and v[2] == 1
+
+
+def test_bench_exits_when_ranks_outnumber_gpus():
+    """An oversubscribed launch (here: 2 local ranks, no visible GPU) exits
+    non-zero with the reason, before any process group or timing."""
+    import subprocess
+    import sys
+    env = dict(os.environ, RANK="1", LOCAL_RANK="1", WORLD_SIZE="2", LOCAL_WORLD_SIZE="2",
+               HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2"],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert r.returncode == 2, r.stderr[-500:]
+    assert "one rank per GPU" in r.stderr or "no GPU" in r.stderr
+    assert not r.stdout.strip()

@@ -164,3 +164,16 @@ def test_final_64bit_bit_count_vs_reference(oracle):
         pytest.skip("oracle/_ref not built (no /root/reference here)")
     for ctx in long_message_contexts():
         assert _final(oracle.lib().oracle_sha1_final, ctx) == _final(ref.SHA1Final, ctx), ctx.totalLength
+
+
+def test_package_mixed_length_law(pkg, golden, oracle):
+    """bench.py's config-5 legs draw lengths from the package's numpy restatement
+    of the length law; it must reproduce the lengths the reference hashed for
+    the golden files (16384 and the 4x batch of 65536), and the oracle's."""
+    import hashlib
+    for key in ("config5", "config5x4"):
+        n = golden[key]["chunks"]
+        ln = pkg.sha1chunk.mixed_lengths(n)
+        assert hashlib.sha1(ln.tobytes()).hexdigest() == golden[key]["lengths_sha1"], key
+        assert int(ln.astype(np.uint64).sum()) == golden[key]["total_bytes"]
+    assert np.array_equal(pkg.sha1chunk.mixed_lengths(2000), oracle.mixed_lengths(2000))
