@@ -134,6 +134,75 @@ int main(void) {
         }
     }
     CHECK(seen == n && sha1chunk_vq_pending(q) == 0, "vq drained %zu of %zu", seen, n);
+    /* zero-copy receive: reserve a buffer in the ring, fill it in place as
+     * DATA packets would (1484-byte pieces, reliable_udp.c:339), commit it,
+     * and release it once its result is back (after the job-buffer copy,
+     * reliable_udp.c:696-709) -- up to 8 buffers outstanding, every 7th
+     * reservation dropped without a commit; the chunk is checked in place
+     * after its result, before the release */
+    {
+        void **bufp = calloc(n, sizeof *bufp);
+        memset(got, 0, n);
+        seen = 0;
+        size_t held = 0;
+        for (size_t i = 0; i < n; ++i) {
+            if (i % 7 == 3) { /* an aborted session */
+                void *b = sha1chunk_vq_reserve(q, L512);
+                CHECK(b != NULL, "vq_reserve (abort): %s", sha1chunk_last_error());
+                CHECK(sha1chunk_vq_release(q, b) == 0, "vq_release (abort)");
+            }
+            uint8_t *b = sha1chunk_vq_reserve(q, len[i] ? len[i] : 1);
+            CHECK(b != NULL, "vq_reserve: %s", sha1chunk_last_error());
+            for (uint32_t o = 0; o < len[i]; o += 1484)
+                memcpy(b + o, buf + off[i] + o, len[i] - o < 1484 ? len[i] - o : 1484);
+            bufp[i] = b;
+            CHECK(sha1chunk_vq_commit(q, b, len[i], exp + 20 * i, i) == 0, "vq_commit: %s", sha1chunk_last_error());
+            ++held;
+            for (;;) {
+                long k = sha1chunk_vq_poll(q, tags, bad, 64, held >= 8);
+                CHECK(k >= 0, "vq_poll: %s", sha1chunk_last_error());
+                for (long j = 0; j < k; ++j) {
+                    const uint64_t t = tags[j];
+                    CHECK(t < n && !got[t], "vq tag");
+                    got[t] = 1;
+                    CHECK(bad[j] == (t == 5 || t == 200), "vq flag %llu", (unsigned long long)t);
+                    CHECK(memcmp(bufp[t], buf + off[t], len[t]) == 0, "reserved buffer changed");
+                    CHECK(sha1chunk_vq_release(q, bufp[t]) == 0, "vq_release");
+                    CHECK(sha1chunk_vq_release(q, bufp[t]) != 0, "double release accepted");
+                    --held;
+                    ++seen;
+                }
+                if (held < 8) break;
+            }
+        }
+        for (;;) {
+            long k = sha1chunk_vq_poll(q, tags, bad, 64, 1);
+            if (k <= 0) break;
+            for (long j = 0; j < k; ++j) {
+                const uint64_t t = tags[j];
+                CHECK(t < n && !got[t], "vq tag");
+                got[t] = 1;
+                CHECK(bad[j] == (t == 5 || t == 200), "vq flag");
+                CHECK(sha1chunk_vq_release(q, bufp[t]) == 0, "vq_release");
+                ++seen;
+            }
+        }
+        CHECK(seen == n && sha1chunk_vq_pending(q) == 0, "vq zero-copy drained %zu of %zu", seen, n);
+        CHECK(sha1chunk_vq_commit(q, buf, 3, exp, 1) != 0, "commit of a foreign buffer accepted");
+        if (mo == 1) {
+            /* the persistent ring (its floor: 2 groups of 64 max-length
+             * chunks, 64 MiB here): reservations never released fill it, and
+             * reserve fails instead of waiting forever */
+            void *hold[256];
+            size_t k = 0;
+            while (k < 256 && (hold[k] = sha1chunk_vq_reserve(q, L512)) != NULL) ++k;
+            CHECK(k >= 126 && k <= 128, "ring of 64 MiB took %zu reservations of 512 KiB", k);
+            for (size_t j = 0; j < k; ++j) CHECK(sha1chunk_vq_release(q, hold[j]) == 0, "vq_release (hold)");
+            void *b = sha1chunk_vq_reserve(q, L512);
+            CHECK(b != NULL && sha1chunk_vq_release(q, b) == 0, "reserve after releasing the ring");
+        }
+        free(bufp);
+    }
     sha1chunk_vq_destroy(q);
     free(got);
     }

@@ -56,20 +56,10 @@ __device__ __forceinline__ constexpr uint32_t round_k() {
 
 // WK = true: wt already holds W[t] + K[t] (the split producer adds it), so
 // e + W + K is a 2-operand v_add_u32 (VOP2, issues ~6% faster than VOP3).
-// RV (A/B, fused kernel): 0 = the sums as two v_add3_u32 (half-rate); 1 =
-// every sum as full-rate VOP2 v_add_u32 (four per round, K as a literal);
-// 2 = e + W + K as two VOP2 adds, the round sum still one add3.
-__device__ __forceinline__ uint32_t add_vop2(uint32_t a, uint32_t b) {
-    uint32_t r;
-    asm("v_add_u32 %0, %1, %2" : "=v"(r) : "v"(a), "v"(b));
-    return r;
-}
-__device__ __forceinline__ uint32_t add_vop2_k(uint32_t a, uint32_t k) {
-    uint32_t r;
-    asm("v_add_u32 %0, %2, %1" : "=v"(r) : "v"(a), "i"(k));
-    return r;
-}
-template <int T, bool WK = false, int RV = 0>
+// (The fused kernel keeps the two v_add3_u32: forms with every sum as a VOP2
+// add were measured no faster, profiles/fused_roundsum_ab_r02.json; their
+// code left the source in round 4.)
+template <int T, bool WK = false>
 __device__ __forceinline__ void round_step(uint32_t (&v)[5], uint32_t wt) {
     constexpr int ia = (5 - (T % 5)) % 5;
     constexpr int ib = (ia + 1) % 5, ic = (ia + 2) % 5, id = (ia + 3) % 5, ie = (ia + 4) % 5;
@@ -90,15 +80,10 @@ __device__ __forceinline__ void round_step(uint32_t (&v)[5], uint32_t wt) {
     uint32_t x;
     if constexpr (WK)
         x = v[ie] + wt;
-    else if constexpr (RV != 0)
-        x = add_vop2_k(add_vop2(v[ie], wt), round_k<T>());
     else
         x = v[ie] + wt + round_k<T>();
     uint32_t t;
-    if constexpr (RV == 1)
-        t = add_vop2(add_vop2(rotl(v[ia], 5), f), x);
-    else
-        asm("v_add3_u32 %0, %1, %2, %3" : "=v"(t) : "v"(rotl(v[ia], 5)), "v"(f), "v"(x));
+    asm("v_add3_u32 %0, %1, %2, %3" : "=v"(t) : "v"(rotl(v[ia], 5)), "v"(f), "v"(x));
     v[ie] = t;
     v[ib] = rotl(v[ib], 30);
 }
@@ -111,7 +96,7 @@ __device__ __forceinline__ uint32_t sched_step(uint32_t (&w)[16]) {
     return x;
 }
 
-template <int T, int RV = 0>
+template <int T>
 struct Rounds {
     __device__ __forceinline__ static void run(uint32_t (&v)[5], uint32_t (&w)[16]) {
         if constexpr (T < 80) {
@@ -120,18 +105,17 @@ struct Rounds {
                 wt = w[T];
             else
                 wt = sched_step<T>(w);
-            round_step<T, false, RV>(v, wt);
-            Rounds<T + 1, RV>::run(v, w);
+            round_step<T, false>(v, wt);
+            Rounds<T + 1>::run(v, w);
         }
     }
 };
 
 // One full compression: h[] <- h[] + F(h[], w[]); w[] holds the block as
 // big-endian words and is consumed (overwritten by the schedule).
-template <int RV = 0>
 __device__ __forceinline__ void compress(uint32_t (&h)[5], uint32_t (&w)[16]) {
     uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
-    Rounds<0, RV>::run(v, w);
+    Rounds<0>::run(v, w);
 #pragma unroll
     for (int i = 0; i < 5; ++i) h[i] += v[i];
 }

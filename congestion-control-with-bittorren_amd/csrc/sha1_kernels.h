@@ -34,6 +34,10 @@ hipError_t launch_fused(const BatchArgs& A, hipStream_t st);
 // flags (2, 3, 8-10, 12, 13, 10*U+V, 500+V, 569, 577-585, 86, 87, 590).
 bool split_unit_built(int unit_blocks);
 hipError_t launch_split(const BatchArgs& A, int unit_blocks, hipStream_t st);
+// The other shapes of the split-kernel study: weak stubs in the product
+// (no such shape), defined by tools/ab_kernels.hip in the A/B library.
+bool split_unit_study_built(int unit_blocks);
+hipError_t launch_split_study(const BatchArgs& A, int unit_blocks, hipStream_t st);
 // Sorted ragged batch of more groups than CUs (A.order set, sorted_len =
 // the lengths in that order): a device-side plan splits the groups between
 // the one-group split shape (longest first) and the fused kernel, or runs

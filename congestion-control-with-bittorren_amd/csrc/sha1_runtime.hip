@@ -1,5 +1,8 @@
-// sha1_runtime.hip -- host runtime of libsha1chunk.so: the C-ABI batch entry
-// points of include/sha1chunk.h.
+// sha1_runtime.hip -- the HIP backend of libsha1chunk.so (built into
+// libsha1chunk_hip.so): the device half of the C-ABI batch entry points of
+// include/sha1chunk.h, exported as s1be_* and reached only through the thin
+// C front end (frontend.c), which dlopen()s this library on the first call
+// that needs the GPU and handles the host small-call paths itself.
 //
 // Per device: one compute stream per pipeline slot, a device arena and a
 // pinned host arena for each of two slots, so that packing/reading batch b+1
@@ -24,13 +27,14 @@
 #include <numeric>
 #include <string>
 #include <thread>
+#include <tuple>
+#include <unordered_map>
 #include <sys/stat.h>
 #include <unistd.h>
 #include <vector>
 
 #include "../../include/sha1chunk.h"
 #include "part_pool.hpp"
-#include "sha1_host.h"
 #include "sha1_kernels.h"
 
 namespace {
@@ -161,6 +165,10 @@ struct Device {
     // threads that pack pageable host chunks into pinned staging (created on
     // the first such batch, alive with the process; idle ones sleep)
     std::unique_ptr<PartPool> pack;
+    // CUs held by the persistent verify-queue drains of this device (under
+    // drain_mu): each drain workgroup takes a whole CU (all of its LDS)
+    std::mutex drain_mu;
+    int drain_cus = 0;
 };
 
 std::once_flag g_once;
@@ -224,21 +232,6 @@ int ensure_copy(Device& D) {
     return SHA1CHUNK_OK;
 }
 
-// SHA1CHUNK_HOST_SMALL=<bytes> (default 0: off): host calls of at most that
-// many bytes -- one chunk from shahash / get_chunk_hash / verify_hash, the
-// streaming trio's updates -- are hashed on the host (sha1_host.c: x86 SHA
-// extensions) instead of as one lane's 6 ms serial chain on the device.
-// Opt-in for latency-bound single-chunk callers (SURVEY.md 7.1 step 2, 8f
-// rank 2); a device is still required, so this is never a fallback.
-uint64_t host_small_bytes() {
-    static const uint64_t b = [] {
-        const char* e = getenv("SHA1CHUNK_HOST_SMALL");
-        return e ? strtoull(e, nullptr, 10) : 0ull;
-    }();
-    return b;
-}
-int require_device();
-
 // Acquire the calling thread's device (initialising it on first use).
 int get_device(Device** out) {
     if (device_count() <= 0) return fail(SHA1CHUNK_ENODEV, "%s", g_probe_err.c_str());
@@ -262,94 +255,6 @@ int get_device(Device** out) {
         }
     }
     *out = &D;
-    return SHA1CHUNK_OK;
-}
-
-// Presence check of the host small-call paths, without starting the HIP
-// runtime (50-250 ms in a fresh process, profiles/startup_r03.json; the
-// whole of make-chunks on a small file otherwise): the kernel driver's KFD
-// topology lists gfx950 agents (gfx_target_version 90500) whose properties
-// and render node this process may open, next to an accessible /dev/kfd,
-// and no such GPU agent of another kind -- probe()'s rule that every device
-// be gfx950.  Agents this process cannot read (a container that exposes one
-// GPU of a node) are not its devices.  A *_VISIBLE_DEVICES mask caps the
-// count at its number of entries.  Returns the device count, 0 when none is
-// visible, or -1 when it cannot tell (no readable topology, an empty mask):
-// then the HIP probe decides.
-std::string g_light_err;
-int light_count() {
-    static std::once_flag once;
-    static int count = -1;
-    std::call_once(once, [] {
-        int masked = 1 << 30;
-        for (const char* v : {"ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES",
-                              "GPU_DEVICE_ORDINAL"}) {
-            const char* m = getenv(v);
-            if (!m) continue;
-            int tokens = 0;
-            for (const char* c = m; *c;) {
-                const char* e = strchr(c, ',');
-                const size_t len = e ? static_cast<size_t>(e - c) : strlen(c);
-                if (len) ++tokens;
-                c += len + (e ? 1 : 0);
-            }
-            if (tokens == 0) return;
-            masked = std::min(masked, tokens);
-        }
-        if (access("/dev/kfd", R_OK | W_OK) != 0) {
-            count = 0;
-            g_light_err = "no HIP device visible (/dev/kfd not accessible)";
-            return;
-        }
-        const char* dir = "/sys/class/kfd/kfd/topology/nodes";
-        int n = 0, readable = 0;
-        for (int node = 0; node < 4096; ++node) {
-            char path[128];
-            snprintf(path, sizeof path, "%s/%d", dir, node);
-            if (access(path, F_OK) != 0) break;
-            snprintf(path, sizeof path, "%s/%d/properties", dir, node);
-            FILE* f = fopen(path, "r");
-            if (!f) continue;  // not this process's agent
-            ++readable;
-            char key[64];
-            unsigned long long val;
-            unsigned long long target = 0, minor = 0;
-            while (fscanf(f, "%63s %llu", key, &val) == 2) {
-                if (!strcmp(key, "gfx_target_version")) target = val;
-                if (!strcmp(key, "drm_render_minor")) minor = val;
-            }
-            fclose(f);
-            if (target == 0) continue;  // a CPU agent
-            snprintf(path, sizeof path, "/dev/dri/renderD%llu", minor);
-            if (access(path, R_OK | W_OK) != 0) continue;
-            if (target != 90500) {
-                count = 0;
-                g_light_err = "a GPU agent is gfx_target_version " + std::to_string(target) +
-                              ", this build targets gfx950 only";
-                return;
-            }
-            ++n;
-        }
-        if (readable == 0) return;
-        count = std::min(n, masked);
-        if (count == 0) g_light_err = "no HIP device visible (no accessible gfx950 agent)";
-    });
-    return count;
-}
-
-// The library's contract for every call, host small-call path included: a
-// gfx950 device is present and the thread's device index is valid.
-int require_device() {
-    const int lc = light_count();
-    if (lc < 0) {
-        if (device_count() <= 0) return fail(SHA1CHUNK_ENODEV, "%s", g_probe_err.c_str());
-        if (t_dev < 0 || t_dev >= g_count) return fail(SHA1CHUNK_EINVAL, "bad device %d", t_dev);
-        return SHA1CHUNK_OK;
-    }
-    if (lc == 0) return fail(SHA1CHUNK_ENODEV, "%s", g_light_err.c_str());
-    int k = lc;  // logical devices, as probe() counts them
-    if (const char* e = getenv("SHA1CHUNK_VIRTUAL_DEVICES")) k = std::max(1, std::min(64, atoi(e)));
-    if (t_dev < 0 || t_dev >= k) return fail(SHA1CHUNK_EINVAL, "bad device %d", t_dev);
     return SHA1CHUNK_OK;
 }
 
@@ -722,13 +627,13 @@ int hash_host_all(const uint8_t* base, const uint64_t* offsets, const uint32_t* 
 // ================================================================ C ABI ====
 extern "C" {
 
-int sha1chunk_device_count(void) {
+int s1be_device_count(void) {
     const int n = device_count();
     if (n <= 0) fail(SHA1CHUNK_ENODEV, "%s", g_probe_err.c_str());
     return n;
 }
 
-int sha1chunk_set_device(int device) {
+int s1be_set_device(int device) {
     const int n = device_count();
     if (n <= 0) return fail(SHA1CHUNK_ENODEV, "%s", g_probe_err.c_str());
     if (device < 0 || device >= n) return fail(SHA1CHUNK_EINVAL, "device %d of %d", device, n);
@@ -736,13 +641,20 @@ int sha1chunk_set_device(int device) {
     return SHA1CHUNK_OK;
 }
 
-int sha1chunk_get_device(void) { return t_dev; }
+const char* s1be_last_error(void) { return t_err.c_str(); }
 
-const char* sha1chunk_last_error(void) { return t_err.c_str(); }
+// PCI address of logical device `device`'s physical GPU (multi-device tests
+// and bench.py's device identity: distinct ranks/threads, distinct GPUs).
+int s1be_device_pci_bus_id(int device, char* buf, size_t len) {
+    const int n = device_count();
+    if (n <= 0) return fail(SHA1CHUNK_ENODEV, "%s", g_probe_err.c_str());
+    if (device < 0 || device >= n) return fail(SHA1CHUNK_EINVAL, "device %d of %d", device, n);
+    if (len > static_cast<size_t>(INT32_MAX)) len = INT32_MAX;
+    HIP_TRY(hipDeviceGetPCIBusId(buf, static_cast<int>(len), g_dev[device].id));
+    return SHA1CHUNK_OK;
+}
 
-const char* sha1chunk_version(void) { return "sha1chunk gfx950: lane,fused,split,mixed"; }
-
-int sha1chunk_hash_device_async(const void* d_base, const uint64_t* d_offsets,
+int s1be_hash_device_async(const void* d_base, const uint64_t* d_offsets,
                                 const uint32_t* d_lengths, size_t n, uint8_t* d_digests,
                                 void* stream, int kernel) {
     if (n > 0xffffffffu) return fail(SHA1CHUNK_EINVAL, "n too large");
@@ -779,7 +691,7 @@ int sha1chunk_hash_device_async(const void* d_base, const uint64_t* d_offsets,
     return rc;
 }
 
-int sha1chunk_hash_uniform_async(const void* d_base, uint32_t chunk_len, size_t n,
+int s1be_hash_uniform_async(const void* d_base, uint32_t chunk_len, size_t n,
                                  uint8_t* d_digests, void* stream, int kernel) {
     if (n > 0xffffffffu) return fail(SHA1CHUNK_EINVAL, "n too large");
     if (n && (!d_base || !d_digests)) return fail(SHA1CHUNK_EINVAL, "null device pointer");
@@ -794,7 +706,7 @@ int sha1chunk_hash_uniform_async(const void* d_base, uint32_t chunk_len, size_t 
     return launch_checked(choose_kernel(kernel, n, D->cus), A, static_cast<hipStream_t>(stream), D->cus);
 }
 
-int sha1chunk_compare_device_async(const uint8_t* d_digests, const uint8_t* d_expected, size_t n,
+int s1be_compare_device_async(const uint8_t* d_digests, const uint8_t* d_expected, size_t n,
                                    uint8_t* d_mismatch, void* stream) {
     if (n > 0xffffffffu) return fail(SHA1CHUNK_EINVAL, "n too large");
     if (n && (!d_digests || !d_expected || !d_mismatch))
@@ -808,28 +720,18 @@ int sha1chunk_compare_device_async(const uint8_t* d_digests, const uint8_t* d_ex
     return SHA1CHUNK_OK;
 }
 
-int sha1chunk_hash_batch(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+int s1be_hash_batch(const void* base, const uint64_t* offsets, const uint32_t* lengths,
                          size_t n, uint8_t* digests, unsigned flags) {
     if (n == 0) return SHA1CHUNK_OK;
     if (!base || !offsets || !lengths || !digests) return fail(SHA1CHUNK_EINVAL, "null pointer");
     if (n > 0xffffffffu) return fail(SHA1CHUNK_EINVAL, "n too large");
-    if (!(flags & SHA1CHUNK_DEVICE) && host_small_bytes()) {
-        uint64_t total = 0;
-        for (size_t i = 0; i < n && total <= host_small_bytes(); ++i) total += lengths[i];
-        if (total <= host_small_bytes()) {
-            if (int rc = require_device()) return rc;
-            const uint8_t* b = static_cast<const uint8_t*>(base);
-            for (size_t i = 0; i < n; ++i) sha1host_digest(b + offsets[i], lengths[i], digests + 20 * i);
-            return SHA1CHUNK_OK;
-        }
-    }
     if (flags & SHA1CHUNK_DEVICE) {
         Device* D;
         int rc = get_device(&D);
         if (rc) return rc;
         std::lock_guard<std::mutex> lk(D->mu);
         hipStream_t st = D->slot[0].stream;
-        if ((rc = sha1chunk_hash_device_async(base, offsets, lengths, n, digests, st,
+        if ((rc = s1be_hash_device_async(base, offsets, lengths, n, digests, st,
                                               SHA1CHUNK_KERNEL_AUTO)))
             return rc;
         HIP_TRY(hipStreamSynchronize(st));
@@ -840,7 +742,7 @@ int sha1chunk_hash_batch(const void* base, const uint64_t* offsets, const uint32
     return hash_host(b, offsets, lengths, n, digests);
 }
 
-int sha1chunk_verify_batch(const void* base, const uint64_t* offsets, const uint32_t* lengths,
+int s1be_verify_batch(const void* base, const uint64_t* offsets, const uint32_t* lengths,
                            size_t n, const uint8_t* expected, uint8_t* mismatch, unsigned flags) {
     if (n == 0) return SHA1CHUNK_OK;
     if (!expected || !mismatch) return fail(SHA1CHUNK_EINVAL, "null pointer");
@@ -851,18 +753,18 @@ int sha1chunk_verify_batch(const void* base, const uint64_t* offsets, const uint
         std::lock_guard<std::mutex> lk(D->mu);
         Slot& s = D->slot[0];
         if ((rc = s.ddig.ensure(n * 20))) return rc;
-        if ((rc = sha1chunk_hash_device_async(base, offsets, lengths, n,
+        if ((rc = s1be_hash_device_async(base, offsets, lengths, n,
                                               static_cast<uint8_t*>(s.ddig.p), s.stream,
                                               SHA1CHUNK_KERNEL_AUTO)))
             return rc;
-        if ((rc = sha1chunk_compare_device_async(static_cast<uint8_t*>(s.ddig.p), expected, n,
+        if ((rc = s1be_compare_device_async(static_cast<uint8_t*>(s.ddig.p), expected, n,
                                                  mismatch, s.stream)))
             return rc;
         HIP_TRY(hipStreamSynchronize(s.stream));
         return SHA1CHUNK_OK;
     }
     std::vector<uint8_t> dig(n * 20);
-    int rc = sha1chunk_hash_batch(base, offsets, lengths, n, dig.data(), flags);
+    int rc = s1be_hash_batch(base, offsets, lengths, n, dig.data(), flags);
     if (rc) return rc;
     for (size_t i = 0; i < n; ++i) mismatch[i] = memcmp(&dig[20 * i], expected + 20 * i, 20) != 0;
     return SHA1CHUNK_OK;
@@ -978,12 +880,7 @@ long hash_stream_sized(sha1chunk_reader_fn reader, void* reader_ctx, sha1chunk_s
 
 extern "C" {
 
-long sha1chunk_hash_stream(sha1chunk_reader_fn reader, void* reader_ctx, sha1chunk_sink_fn sink,
-                           void* sink_ctx) {
-    return hash_stream_sized(reader, reader_ctx, sink, sink_ctx, 0);
-}
-
-long sha1chunk_hash_stream_sized(sha1chunk_reader_fn reader, void* reader_ctx,
+long s1be_hash_stream_sized(sha1chunk_reader_fn reader, void* reader_ctx,
                                  sha1chunk_sink_fn sink, void* sink_ctx, uint64_t size_hint) {
     return hash_stream_sized(reader, reader_ctx, sink, sink_ctx, size_hint);
 }
@@ -1118,41 +1015,8 @@ long hash_file_devices(int fd, off_t pos, off_t end, int nd, int read_threads, F
 }
 }  // namespace
 
-namespace {
-// A regular file of at most SHA1CHUNK_HOST_SMALL bytes (make-chunks on a small
-// file, BASELINE config 1's tmp/C.tar): read and hashed on the host chunk by
-// chunk, as the reference's fread + shahash loop does (chunk.c:15-27), with
-// no pinned slots, streams or code object to set up.  Opt-in like the other
-// small calls; the device must still be present (the caller checked).
-long hash_file_host(int fd, off_t pos, off_t end, FdSink* sk) {
-    std::vector<uint8_t> buf(SHA1CHUNK_CHUNK_LEN);
-    long n = 0;
-    while (pos < end) {
-        const size_t want = static_cast<size_t>(std::min<off_t>(SHA1CHUNK_CHUNK_LEN, end - pos));
-        size_t got = 0;
-        while (got < want) {
-            const ssize_t r = pread(fd, buf.data() + got, want - got, pos + static_cast<off_t>(got));
-            if (r < 0) {
-                if (errno == EINTR) continue;
-                return fail(SHA1CHUNK_EIO, "file read error");
-            }
-            if (r == 0) break;  // the file shrank under us
-            got += static_cast<size_t>(r);
-        }
-        if (got == 0) break;
-        uint8_t dig[20];
-        sha1host_digest(buf.data(), got, dig);
-        fd_sink(sk, static_cast<size_t>(n), dig, 1);
-        ++n;
-        pos += static_cast<off_t>(got);
-        if (got < want) break;
-    }
-    (void)lseek(fd, pos, SEEK_SET);
-    return n;
-}
-}  // namespace
 
-long sha1chunk_hash_fd(int fd, uint8_t* digests, size_t max_chunks, size_t* total_chunks) {
+long s1be_hash_fd(int fd, uint8_t* digests, size_t max_chunks, size_t* total_chunks) {
     FdSink sk{digests, max_chunks};
     struct stat st;
     const off_t pos = lseek(fd, 0, SEEK_CUR);
@@ -1161,12 +1025,8 @@ long sha1chunk_hash_fd(int fd, uint8_t* digests, size_t max_chunks, size_t* tota
         const char* e = getenv("SHA1CHUNK_READ_THREADS");
         const int read_threads = e ? std::max(1, atoi(e)) : 8;
         const off_t end = std::max(pos, st.st_size);
-        const bool host = host_small_bytes() && static_cast<uint64_t>(end - pos) <= host_small_bytes();
-        const int nd = host ? 1 : file_devices(static_cast<uint64_t>(end - pos));
-        if (host) {
-            if (int rc = require_device()) return rc;
-            n = hash_file_host(fd, pos, end, &sk);
-        } else if (nd > 1) {
+        const int nd = file_devices(static_cast<uint64_t>(end - pos));
+        if (nd > 1) {
             n = hash_file_devices(fd, pos, end, nd, read_threads, &sk);
         } else {
             PartPool pool(read_threads - 1);
@@ -1175,22 +1035,17 @@ long sha1chunk_hash_fd(int fd, uint8_t* digests, size_t max_chunks, size_t* tota
             (void)lseek(fd, f.pos, SEEK_SET);
         }
     } else {
-        n = sha1chunk_hash_stream(fd_reader, &fd, fd_sink, &sk);
+        n = hash_stream_sized(fd_reader, &fd, fd_sink, &sk, 0);
     }
     if (n < 0) return n;
     if (total_chunks) *total_chunks = static_cast<size_t>(n);
     return static_cast<long>(std::min(static_cast<size_t>(n), max_chunks));
 }
 
-int sha1chunk_compress_blocks(uint32_t state[5], const void* blocks, size_t nblocks) {
+int s1be_compress_blocks(uint32_t state[5], const void* blocks, size_t nblocks) {
     if (!state || (nblocks && !blocks)) return fail(SHA1CHUNK_EINVAL, "null pointer");
     if (nblocks == 0) return SHA1CHUNK_OK;
     if (nblocks * 64 > 0xffffffffull) return fail(SHA1CHUNK_EINVAL, "too many blocks");
-    if (nblocks * 64 <= host_small_bytes()) {
-        if (int rc = require_device()) return rc;
-        sha1host_compress(state, blocks, nblocks);
-        return SHA1CHUNK_OK;
-    }
     Device* D;
     int rc = get_device(&D);
     if (rc) return rc;
@@ -1216,15 +1071,10 @@ int sha1chunk_compress_blocks(uint32_t state[5], const void* blocks, size_t nblo
     return SHA1CHUNK_OK;
 }
 
-int sha1chunk_finish(const uint32_t state[5], uint64_t prefix_bytes, const void* tail,
+int s1be_finish(const uint32_t state[5], uint64_t prefix_bytes, const void* tail,
                      uint32_t tail_len, uint8_t digest[20]) {
     if (!state || !digest || (tail_len && !tail) || tail_len >= 64)
         return fail(SHA1CHUNK_EINVAL, "bad argument");
-    if (host_small_bytes()) {
-        if (int rc = require_device()) return rc;
-        sha1host_finish(state, prefix_bytes, tail, tail_len, digest);
-        return SHA1CHUNK_OK;
-    }
     Device* D;
     int rc = get_device(&D);
     if (rc) return rc;
@@ -1250,7 +1100,7 @@ int sha1chunk_finish(const uint32_t state[5], uint64_t prefix_bytes, const void*
     return SHA1CHUNK_OK;
 }
 
-int sha1chunk_synth_fill_async(void* d_dst, uint64_t first, uint64_t count, uint32_t chunk_len,
+int s1be_synth_fill_async(void* d_dst, uint64_t first, uint64_t count, uint32_t chunk_len,
                                uint64_t seed, void* stream) {
     if (count && !d_dst) return fail(SHA1CHUNK_EINVAL, "null pointer");
     if ((reinterpret_cast<uintptr_t>(d_dst) & 7u) || (chunk_len & 7u && count > 1))
@@ -1264,7 +1114,7 @@ int sha1chunk_synth_fill_async(void* d_dst, uint64_t first, uint64_t count, uint
     return SHA1CHUNK_OK;
 }
 
-int sha1chunk_synth_fill_ragged_async(void* d_base, const uint64_t* d_offsets,
+int s1be_synth_fill_ragged_async(void* d_base, const uint64_t* d_offsets,
                                       const uint32_t* d_lengths, uint64_t first, uint64_t count,
                                       uint64_t seed, void* stream) {
     if (count && (!d_base || !d_offsets || !d_lengths)) return fail(SHA1CHUNK_EINVAL, "null pointer");
@@ -1313,11 +1163,8 @@ namespace {
 struct Pvq;
 }
 
-struct sha1chunk_vq {
+struct s1be_vq {
     Pvq* pv = nullptr;  // the persistent drain (default), or null: batch launches (SHA1CHUNK_VQ_MODE=batch)
-    // batch size 1 with SHA1CHUNK_HOST_SMALL >= max_chunk_len: every submit
-    // is hashed and compared on the host at once (no sets, no drain)
-    bool host1 = false;
     int dev = 0;
     int cus = 256;
     size_t batch = 0;  // launch threshold
@@ -1330,17 +1177,20 @@ struct sha1chunk_vq {
     std::deque<std::pair<uint64_t, uint8_t>> ready;
     size_t pending = 0;
     PartPool* copier = nullptr;
+    std::mutex mu;  // every entry point holds it: a queue may be shared by threads
+    // batch mode's reservations: buffer -> (length, storage)
+    std::unordered_map<void*, std::pair<uint32_t, std::unique_ptr<uint8_t[]>>> reserved;
 };
 
 namespace {
 
-uint64_t* vq_off(sha1chunk_vq*, uint8_t* base) { return reinterpret_cast<uint64_t*>(base); }  // offsets lead the set
-uint32_t* vq_len(sha1chunk_vq* q, uint8_t* base) {
+uint64_t* vq_off(s1be_vq*, uint8_t* base) { return reinterpret_cast<uint64_t*>(base); }  // offsets lead the set
+uint32_t* vq_len(s1be_vq* q, uint8_t* base) {
     return reinterpret_cast<uint32_t*>(base + q->cap * 8);
 }
-uint8_t* vq_exp(sha1chunk_vq* q, uint8_t* base) { return base + q->cap * 12; }
+uint8_t* vq_exp(s1be_vq* q, uint8_t* base) { return base + q->cap * 12; }
 
-int vq_launch(sha1chunk_vq* q, int which) {
+int vq_launch(s1be_vq* q, int which) {
     VqSet& S = q->set[which];
     if (S.count == 0) return SHA1CHUNK_OK;
     HIP_TRY(hipSetDevice(q->dev));
@@ -1367,7 +1217,7 @@ int vq_launch(sha1chunk_vq* q, int which) {
 }
 
 // Move the oldest launched set's results to `ready` (blocking on it).
-int vq_collect_oldest(sha1chunk_vq* q) {
+int vq_collect_oldest(s1be_vq* q) {
     if (q->flight.empty()) return SHA1CHUNK_OK;
     const int which = q->flight.front();
     VqSet& S = q->set[which];
@@ -1383,7 +1233,7 @@ int vq_collect_oldest(sha1chunk_vq* q) {
 
 // Collect every launched set that has finished, oldest first, without
 // blocking.
-int vq_reap(sha1chunk_vq* q) {
+int vq_reap(s1be_vq* q) {
     while (!q->flight.empty()) {
         hipError_t e = hipEventQuery(q->set[q->flight.front()].done);
         if (e == hipErrorNotReady) break;
@@ -1400,7 +1250,7 @@ int vq_reap(sha1chunk_vq* q) {
 // finishes.  Every launch costs at
 // least one chunk's serial hash time (~6 ms), so while the device is busy a
 // bigger batch is free throughput; while it is idle, `batch` bounds latency.
-int vq_maybe_launch(sha1chunk_vq* q) {
+int vq_maybe_launch(s1be_vq* q) {
     VqSet& S = q->set[q->fill];
     // only at whole multiples of `batch`: a caller that submits whole batches
     // still gets every result back through non-blocking polls, no flush
@@ -1414,7 +1264,7 @@ int vq_maybe_launch(sha1chunk_vq* q) {
 }
 
 // ------------------------------------------------ persistent verify queue --
-// sha1chunk_vq with a persistent drain kernel (sha1_vq_drain_kernel): the
+// s1be_vq with a persistent drain kernel (sha1_vq_drain_kernel): the
 // host copies each submitted chunk into a ring in pinned, uncached host
 // memory, writes its length and expected digest next to it, and publishes
 // groups of up to 64 chunks by bumping `pub`.  The drain -- one workgroup
@@ -1434,7 +1284,17 @@ int vq_maybe_launch(sha1chunk_vq* q) {
 // other kernels, which could not share a CU with a drain workgroup (it holds
 // the CU's whole LDS).
 // Positions in both rings are monotonic counters (physical = counter mod
-// ring size); a group never wraps either ring.
+// ring size).  A group is a run of consecutive slots that never wraps the
+// slot ring; each slot points at its chunk's region of the data ring, a
+// region never wraps the data ring, and regions are freed in allocation
+// order (the data ring's head is the oldest region still held).
+// Zero-copy receive (sha1chunk_vq_reserve / commit / release): the caller
+// fills a region in place -- the peer's session buffer (reliable_udp.c:121,
+// filled at :339) -- and commits it, which gives it a slot; the region stays
+// the caller's after its result is collected, until the caller releases it
+// (after copying the verified chunk into its job buffer, reliable_udp.c:
+// 696-709).  A submitted (copied) chunk's region is freed when its result
+// is collected.
 constexpr uint32_t kPvqMaxGroup = 64;
 struct PvqCtl {
     uint32_t pub;   // groups published (host store, release)
@@ -1446,8 +1306,15 @@ struct PvqGroup {
     uint64_t g;         // group index
     uint64_t slot0;     // first slot (monotonic)
     uint32_t count;
-    uint64_t byte_end;  // byte ring position after its last chunk (monotonic)
     bool collected;
+};
+// A byte range of the data ring [start, end) (monotonic positions).
+struct PvqRegion {
+    uint64_t start, end;
+    bool reserved;   // handed out by reserve(): freed by release()
+    bool committed;  // a slot refers to it: its result is pending until collected
+    bool collected;
+    bool released;
 };
 struct Pvq {
     int dev = 0, cus = 256;  // cus: the drain's workgroups (one per CU)
@@ -1470,6 +1337,10 @@ struct Pvq {
     // device memory: digest scratch + the claim counter
     uint8_t* dmem = nullptr;
     std::vector<uint64_t> tags;
+    std::vector<uint64_t> slot_reg;  // per slot: its region's id
+    std::deque<PvqRegion> regions;   // allocated, not yet freed, oldest first
+    uint64_t reg_base = 0;           // id of regions.front()
+    std::unordered_map<uint64_t, uint64_t> held;  // reserved regions not released: ring offset -> id
     uint64_t slot_head = 0, slot_tail = 0, byte_head = 0, byte_tail = 0;
     uint64_t open_slot0 = 0;
     uint32_t open_count = 0;
@@ -1484,6 +1355,9 @@ struct Pvq {
     hipEvent_t ended[2] = {nullptr, nullptr};
     bool launched[2] = {false, false};
     PartPool* copier = nullptr;
+    size_t hbytes = 0;
+    unsigned hflags = 0;
+    int budget_dev = -1;  // device whose drain CU budget this queue holds (pvq_create)
 };
 
 uint64_t env_u64(const char* name, uint64_t dflt) {
@@ -1548,13 +1422,30 @@ int pvq_publish(Pvq* P) {
     const uint32_t gi = static_cast<uint32_t>(g % P->nslots);
     P->grp[2 * gi] = static_cast<uint32_t>(P->open_slot0 % P->nslots);
     P->grp[2 * gi + 1] = P->open_count;
-    P->groups.push_back(PvqGroup{g, P->open_slot0, P->open_count, P->byte_tail, false});
+    P->groups.push_back(PvqGroup{g, P->open_slot0, P->open_count, false});
     ++P->inflight;
     P->open_slot0 = P->slot_tail;
     P->open_count = 0;
     // the group's bytes, lengths, digests and descriptor are written: release them
     __atomic_store_n(&P->ctl->pub, static_cast<uint32_t>(g + 1), __ATOMIC_RELEASE);
     return pvq_ensure_drain(P);
+}
+
+// A region is free once nothing refers to it: a copied chunk once its
+// result is collected; a reserved one once the caller released it and its
+// result (if it was committed) is collected.
+bool region_free(const PvqRegion& r) {
+    if (!r.reserved) return r.collected;
+    return r.released && (r.collected || !r.committed);
+}
+
+// Free the oldest regions that are free; the data ring's head follows.
+void pvq_free_regions(Pvq* P) {
+    while (!P->regions.empty() && region_free(P->regions.front())) {
+        P->regions.pop_front();
+        ++P->reg_base;
+    }
+    P->byte_head = P->regions.empty() ? P->byte_tail : P->regions.front().start;
 }
 
 // Collect finished groups (in any order) and free ring space up to the
@@ -1574,35 +1465,47 @@ int pvq_reap(Pvq* P) {
         for (uint32_t j = 0; j < G.count; ++j) {
             const uint64_t sl = (G.slot0 + j) % P->nslots;
             P->ready.emplace_back(P->tags[sl], P->res[sl]);
+            P->regions[P->slot_reg[sl] - P->reg_base].collected = true;
         }
         G.collected = true;
         --P->inflight;
     }
     while (!P->groups.empty() && P->groups.front().collected) {
         P->slot_head = P->groups.front().slot0 + P->groups.front().count;
-        P->byte_head = P->groups.front().byte_end;
         P->groups.pop_front();
     }
-    if (P->groups.empty()) {
-        P->slot_head = P->open_slot0;
-        if (P->open_count == 0) P->byte_head = P->byte_tail;
-    }
+    if (P->groups.empty()) P->slot_head = P->open_slot0;
+    pvq_free_regions(P);
     return SHA1CHUNK_OK;
 }
 
+int pvq_publish(Pvq* P);
+
 // Wait (bounded) until `pred` holds, reaping and keeping a drain alive.
-template <typename Pred>
-int pvq_wait(Pvq* P, Pred pred, const char* what) {
+// An open group is published first (its chunks hold ring space too), and a
+// wait that only the caller can end -- the oldest region of the data ring
+// is a reserved buffer not yet committed, or collected and not released --
+// fails at once when `stuck` says so.
+template <typename Pred, typename Stuck>
+int pvq_wait(Pvq* P, Pred pred, const char* what, Stuck stuck) {
     const auto t0 = std::chrono::steady_clock::now();
     int rc;
     for (;;) {
         if ((rc = pvq_reap(P))) return rc;
         if (pred()) return SHA1CHUNK_OK;
+        if (P->open_count && (rc = pvq_publish(P))) return rc;
+        if (stuck())
+            return fail(SHA1CHUNK_ENOMEM, "vq: %s: the ring is held by %zu reserved buffers not released",
+                        what, P->held.size());
         if (P->inflight && (rc = pvq_ensure_drain(P))) return rc;
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
             return fail(SHA1CHUNK_EHIP, "vq: %s timed out (drain not progressing)", what);
         std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
+}
+template <typename Pred>
+int pvq_wait(Pvq* P, Pred pred, const char* what) {
+    return pvq_wait(P, pred, what, [] { return false; });
 }
 
 // Queues alive at process exit (a caller that never destroys its queue):
@@ -1628,6 +1531,64 @@ void pvq_track(Pvq* P, bool add) {
         v.erase(std::remove(v.begin(), v.end(), P), v.end());
 }
 
+// Pinned rings of destroyed queues, kept for the next queue of the same
+// size: hipHostFree (like hipFree) can wait for the whole device, i.e. for
+// other threads' busy drains, so a queue's destroy never frees its ring.
+std::mutex g_ring_mu;
+std::vector<std::tuple<uint8_t*, size_t, unsigned>> g_ring_cache;
+constexpr size_t kRingCacheMax = 8;
+
+uint8_t* ring_get(size_t bytes, unsigned flags) {
+    {
+        std::lock_guard<std::mutex> lk(g_ring_mu);
+        for (size_t i = 0; i < g_ring_cache.size(); ++i)
+            if (std::get<1>(g_ring_cache[i]) == bytes && std::get<2>(g_ring_cache[i]) == flags) {
+                uint8_t* p = std::get<0>(g_ring_cache[i]);
+                g_ring_cache.erase(g_ring_cache.begin() + i);
+                return p;
+            }
+    }
+    void* p = nullptr;
+    if (hipHostMalloc(&p, bytes, flags) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return static_cast<uint8_t*>(p);
+}
+
+void ring_put(uint8_t* p, size_t bytes, unsigned flags) {
+    std::lock_guard<std::mutex> lk(g_ring_mu);
+    if (g_ring_cache.size() < kRingCacheMax) {
+        g_ring_cache.emplace_back(p, bytes, flags);
+        return;
+    }
+    (void)hipHostFree(p);  // beyond the cache: rare (more than kRingCacheMax queues destroyed at once)
+}
+
+// Share of the device's CUs a drain takes (SHA1CHUNK_VQ_CUS, default 64),
+// within a per-device budget for all drains (SHA1CHUNK_VQ_CU_BUDGET,
+// default half the CUs) so that queues never hold every CU: a drain
+// workgroup takes a whole CU while its queue is busy, and a process's hash
+// kernels and other queues need the rest.  0 when the budget is spent.
+int drain_cus_take(Device* D) {
+    const int want = static_cast<int>(
+        std::max<uint64_t>(1, std::min<uint64_t>({static_cast<uint64_t>(D->cus), 1024, env_u64("SHA1CHUNK_VQ_CUS", 64)})));
+    const int budget = static_cast<int>(std::min<uint64_t>(
+        static_cast<uint64_t>(D->cus), env_u64("SHA1CHUNK_VQ_CU_BUDGET", static_cast<uint64_t>(D->cus / 2))));
+    std::lock_guard<std::mutex> lk(D->drain_mu);
+    const int left = budget - D->drain_cus;
+    const int take = std::min(want, left);
+    if (take < std::min(want, 8)) return 0;  // too few left to be worth a drain
+    D->drain_cus += take;
+    return take;
+}
+
+void drain_cus_give(int dev, int cus) {
+    if (dev < 0 || dev >= g_count) return;
+    std::lock_guard<std::mutex> lk(g_dev[dev].drain_mu);
+    g_dev[dev].drain_cus -= cus;
+}
+
 void pvq_destroy(Pvq* P) {
     if (!P) return;
     pvq_track(P, false);
@@ -1636,22 +1597,34 @@ void pvq_destroy(Pvq* P) {
         __atomic_store_n(&P->ctl->stop, 1u, __ATOMIC_RELEASE);
         __atomic_thread_fence(__ATOMIC_SEQ_CST);
     }
+    // stream-ordered: waits for this queue's drains only, never the device
+    if (P->dmem && P->stream[0]) (void)hipFreeAsync(P->dmem, P->stream[0]);
     for (int k = 0; k < 2; ++k) {
         if (P->stream[k]) (void)hipStreamSynchronize(P->stream[k]);
         if (P->ended[k]) (void)hipEventDestroy(P->ended[k]);
         if (P->stream[k]) (void)hipStreamDestroy(P->stream[k]);
     }
-    if (P->dmem) (void)hipFree(P->dmem);
-    if (P->hmem) (void)hipHostFree(P->hmem);
+    if (P->hmem) ring_put(P->hmem, P->hbytes, P->hflags);
+    drain_cus_give(P->budget_dev, P->cus);
     delete P->copier;
     delete P;
 }
 
-Pvq* pvq_create(Device* D, size_t batch, uint32_t max_chunk_len) {
+// Ring memory (SHA1CHUNK_VQ_RING_MEM): "uncached" (default) or "coherent"
+// pinned host memory; the drain reads it over PCIe while the host writes.
+unsigned ring_flags() {
+    const char* e = getenv("SHA1CHUNK_VQ_RING_MEM");
+    return e && !strcmp(e, "coherent") ? hipHostMallocCoherent : hipHostMallocUncached;
+}
+
+// The device's logical index for D (the CU budget lives there).
+int device_index(Device* D) { return static_cast<int>(D - g_dev); }
+
+Pvq* pvq_create(Device* D, size_t batch, uint32_t max_chunk_len, int cus) {
     auto* P = new Pvq();
     P->dev = D->id;
-    P->cus = static_cast<int>(std::max<uint64_t>(
-        1, std::min<uint64_t>({static_cast<uint64_t>(D->cus), 1024, env_u64("SHA1CHUNK_VQ_CUS", 64)})));
+    P->cus = cus;
+    P->budget_dev = device_index(D);
     P->maxlen = max_chunk_len;
     P->group_max = static_cast<uint32_t>(std::min<size_t>(batch, kPvqMaxGroup));
     P->idle_ticks = env_u64("SHA1CHUNK_VQ_IDLE_MS", 20) * 100000ull;  // s_memrealtime: 100 MHz
@@ -1663,17 +1636,14 @@ Pvq* pvq_create(Device* D, size_t batch, uint32_t max_chunk_len) {
         std::max<uint64_t>(P->nbytes / std::max<uint64_t>(kAlign, stride / 4), 4 * kPvqMaxGroup), 1u << 20));
     const size_t ns = P->nslots;
     const size_t meta = round_up(ns * 45, 4096);  // off 8, grp 8, len 4, done 4, exp 20, res 1
-    const size_t hbytes = P->nbytes + meta + sizeof(PvqCtl);
-    if (hipHostMalloc(reinterpret_cast<void**>(&P->hmem), hbytes, hipHostMallocUncached) != hipSuccess) {
-        (void)hipGetLastError();
-        P->hmem = nullptr;
-        if (hipHostMalloc(reinterpret_cast<void**>(&P->hmem), hbytes, hipHostMallocCoherent) != hipSuccess) {
-            (void)hipGetLastError();
-            P->hmem = nullptr;
-            fail(SHA1CHUNK_ENOMEM, "vq: pinned ring of %zu bytes", hbytes);
-            pvq_destroy(P);
-            return nullptr;
-        }
+    P->hbytes = P->nbytes + meta + sizeof(PvqCtl);
+    P->hflags = ring_flags();
+    if (!(P->hmem = ring_get(P->hbytes, P->hflags)) &&
+        (P->hflags == hipHostMallocCoherent ||
+         !(P->hmem = ring_get(P->hbytes, P->hflags = hipHostMallocCoherent)))) {
+        fail(SHA1CHUNK_ENOMEM, "vq: pinned ring of %zu bytes", P->hbytes);
+        pvq_destroy(P);
+        return nullptr;
     }
     memset(P->hmem + P->nbytes, 0, meta + sizeof(PvqCtl));
     uint8_t* m = P->hmem + P->nbytes;
@@ -1686,12 +1656,10 @@ Pvq* pvq_create(Device* D, size_t batch, uint32_t max_chunk_len) {
     P->res = m + ns * 44;
     P->ctl = reinterpret_cast<PvqCtl*>(P->hmem + P->nbytes + meta);
     P->tags.assign(ns, 0);
-    if (hipMalloc(reinterpret_cast<void**>(&P->dmem), 20ull * ns + 256) != hipSuccess ||
-        hipMemset(P->dmem + 20ull * ns, 0, 256) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
-        fail(SHA1CHUNK_ENOMEM, "vq: device scratch");
-        pvq_destroy(P);
-        return nullptr;
-    }
+    P->slot_reg.assign(ns, 0);
+    // streams first: the device scratch is allocated and cleared in stream
+    // order on stream 0, so creating a queue never waits for the whole device
+    // (other threads' drains and batches)
     for (int k = 0; k < 2; ++k)
         if (hipStreamCreateWithFlags(&P->stream[k], hipStreamNonBlocking) != hipSuccess ||
             hipEventCreateWithFlags(&P->ended[k], hipEventDisableTiming) != hipSuccess) {
@@ -1699,6 +1667,14 @@ Pvq* pvq_create(Device* D, size_t batch, uint32_t max_chunk_len) {
             pvq_destroy(P);
             return nullptr;
         }
+    if (hipMallocAsync(reinterpret_cast<void**>(&P->dmem), 20ull * ns + 256, P->stream[0]) != hipSuccess ||
+        hipMemsetAsync(P->dmem + 20ull * ns, 0, 256, P->stream[0]) != hipSuccess ||
+        hipStreamSynchronize(P->stream[0]) != hipSuccess) {
+        (void)hipGetLastError();
+        fail(SHA1CHUNK_ENOMEM, "vq: device scratch");
+        pvq_destroy(P);
+        return nullptr;
+    }
     P->copier = new PartPool(vq_copy_helpers());
     pvq_track(P, true);
     return P;
@@ -1717,33 +1693,99 @@ void pvq_stop_all_at_exit() {
     }
 }
 
-int pvq_submit(Pvq* P, const void* chunk, uint32_t len, const uint8_t expected[20], uint64_t tag) {
+// Room for `len` bytes in the data ring (a region never wraps it): a bounded
+// wait while in-flight groups can free space.  Returns the new region's id.
+int pvq_alloc(Pvq* P, uint32_t len, bool reserved, uint64_t* id) {
     const uint64_t need = round_up(std::max<uint32_t>(len, 1), kAlign);
-    int rc;
-    // a group never wraps a ring: close it where either ring wraps
-    const bool slot_wrap = P->slot_tail != 0 && (P->slot_tail % P->nslots) == 0;
-    const bool byte_wrap = (P->byte_tail % P->nbytes) + need > P->nbytes;
-    if ((slot_wrap || byte_wrap) && (rc = pvq_publish(P))) return rc;
-    const uint64_t pos = byte_wrap ? P->byte_tail + (P->nbytes - P->byte_tail % P->nbytes) : P->byte_tail;
-    // room in both rings (a bounded wait for the drain to free some)
-    if ((rc = pvq_wait(P, [&] {
-             return P->slot_tail + 1 - P->slot_head <= P->nslots && pos + need - P->byte_head <= P->nbytes;
-         }, "submit (ring full)")))
+    auto pos = [&] {
+        const uint64_t t = P->byte_tail;
+        return (t % P->nbytes) + need > P->nbytes ? t + (P->nbytes - t % P->nbytes) : t;
+    };
+    auto stuck = [&] {
+        if (P->regions.empty()) return false;
+        const PvqRegion& r = P->regions.front();
+        return r.reserved && !r.released && (!r.committed || r.collected);
+    };
+    if (int rc = pvq_wait(P, [&] { return pos() + need - P->byte_head <= P->nbytes; }, "data ring full", stuck))
         return rc;
+    const uint64_t at = pos();
+    P->regions.push_back(PvqRegion{at, at + need, reserved, false, false, false});
+    P->byte_tail = at + need;
+    *id = P->reg_base + P->regions.size() - 1;
+    return SHA1CHUNK_OK;
+}
+
+// Give region `id` (filled, `len` bytes) the next slot, with its expected
+// digest and tag, and publish when the group is full or the device idle.
+int pvq_enqueue(Pvq* P, uint64_t id, uint32_t len, const uint8_t expected[20], uint64_t tag) {
+    int rc;
+    // a group never wraps the slot ring: close it where the ring wraps
+    if (P->slot_tail != 0 && (P->slot_tail % P->nslots) == 0 && (rc = pvq_publish(P))) return rc;
+    if ((rc = pvq_wait(P, [&] { return P->slot_tail + 1 - P->slot_head <= P->nslots; }, "slot ring full")))
+        return rc;
+    PvqRegion& r = P->regions[id - P->reg_base];
     const uint64_t sl = P->slot_tail % P->nslots;
-    const uint64_t at = pos % P->nbytes;
-    if (len) pool_copy(*P->copier, P->data + at, static_cast<const uint8_t*>(chunk), len);
-    P->off[sl] = at;
+    P->off[sl] = r.start % P->nbytes;
     P->len[sl] = len;
     memcpy(P->exp + 20 * sl, expected, 20);
     P->tags[sl] = tag;
+    P->slot_reg[sl] = id;
+    r.committed = true;
     if (P->open_count == 0) P->open_slot0 = P->slot_tail;
     ++P->open_count;
     ++P->slot_tail;
-    P->byte_tail = pos + need;
     ++P->pending;
     if ((rc = pvq_reap(P))) return rc;
     if (P->open_count >= P->group_max || P->inflight < static_cast<size_t>(P->cus)) return pvq_publish(P);
+    return SHA1CHUNK_OK;
+}
+
+int pvq_submit(Pvq* P, const void* chunk, uint32_t len, const uint8_t expected[20], uint64_t tag) {
+    uint64_t id;
+    if (int rc = pvq_alloc(P, len, false, &id)) return rc;
+    if (len)
+        pool_copy(*P->copier, P->data + P->regions[id - P->reg_base].start % P->nbytes,
+                  static_cast<const uint8_t*>(chunk), len);
+    return pvq_enqueue(P, id, len, expected, tag);
+}
+
+void* pvq_reserve(Pvq* P, uint32_t len) {
+    uint64_t id;
+    if (pvq_alloc(P, len, true, &id)) return nullptr;
+    const uint64_t at = P->regions[id - P->reg_base].start % P->nbytes;
+    P->held[at] = id;
+    return P->data + at;
+}
+
+// The reserved region `buf` points at (its id), or fails.
+int pvq_held(Pvq* P, const void* buf, uint64_t* id) {
+    const uint8_t* b = static_cast<const uint8_t*>(buf);
+    if (b < P->data || b >= P->data + P->nbytes)
+        return fail(SHA1CHUNK_EINVAL, "vq: %p is not a buffer of this queue", buf);
+    auto it = P->held.find(static_cast<uint64_t>(b - P->data));
+    if (it == P->held.end())
+        return fail(SHA1CHUNK_EINVAL, "vq: %p is not a reserved buffer (released already?)", buf);
+    *id = it->second;
+    return SHA1CHUNK_OK;
+}
+
+int pvq_commit(Pvq* P, void* buf, uint32_t len, const uint8_t expected[20], uint64_t tag) {
+    uint64_t id;
+    if (int rc = pvq_held(P, buf, &id)) return rc;
+    const PvqRegion& r = P->regions[id - P->reg_base];
+    if (r.committed) return fail(SHA1CHUNK_EINVAL, "vq: buffer %p committed twice", buf);
+    if (len > r.end - r.start)
+        return fail(SHA1CHUNK_EINVAL, "vq: commit of %u bytes into a %llu-byte reservation", len,
+                    static_cast<unsigned long long>(r.end - r.start));
+    return pvq_enqueue(P, id, len, expected, tag);
+}
+
+int pvq_release(Pvq* P, void* buf) {
+    uint64_t id;
+    if (int rc = pvq_held(P, buf, &id)) return rc;
+    P->held.erase(static_cast<uint64_t>(static_cast<uint8_t*>(buf) - P->data));
+    P->regions[id - P->reg_base].released = true;
+    pvq_free_regions(P);
     return SHA1CHUNK_OK;
 }
 
@@ -1776,79 +1818,10 @@ size_t vq_cap(size_t batch) {
     return std::max(batch, std::min(4 * batch, 512 / batch * batch));  // a multiple of batch
 }
 
-}  // namespace
-
-extern "C" {
-
-sha1chunk_vq* sha1chunk_vq_create(size_t batch, uint32_t max_chunk_len) {
-    if (batch == 0 || batch > (1u << 20) || max_chunk_len == 0) {
-        fail(SHA1CHUNK_EINVAL, "vq: batch 1..2^20 and max_chunk_len > 0 required");
-        return nullptr;
-    }
-    // The batch-size-1 host path ("keep the CPU path for
-    // batch size 1"): a peer verifying one chunk at a time, as
-    // packet_handler.c:472 -> job.c:217 does, would otherwise wait for one
-    // lane's serial chain (~6 ms per 512 KiB) per chunk.  Opt-in through the
-    // same knob as the other one-chunk calls; a device is still required.
-    if (batch == 1 && max_chunk_len <= host_small_bytes()) {
-        if (require_device()) return nullptr;
-        auto* q = new sha1chunk_vq();
-        q->host1 = true;
-        q->batch = q->cap = 1;
-        q->maxlen = max_chunk_len;
-        return q;
-    }
-    Device* D;
-    if (get_device(&D)) return nullptr;
-    auto* q = new sha1chunk_vq();
-    q->dev = D->id;
-    // the persistent drain unless SHA1CHUNK_VQ_MODE=batch (launch per batch)
-    const char* mode = getenv("SHA1CHUNK_VQ_MODE");
-    if (!(mode && !strcmp(mode, "batch"))) {
-        q->pv = pvq_create(D, batch, max_chunk_len);
-        if (!q->pv) {
-            delete q;
-            return nullptr;
-        }
-        return q;
-    }
-    q->cus = D->cus;
-    q->batch = batch;
-    q->cap = vq_cap(batch);
-    q->maxlen = max_chunk_len;
-    q->stride = round_up(max_chunk_len, kAlign);
-    q->meta = round_up(q->cap * (8 + 4 + 20), kAlign);
-    q->copier = new PartPool(vq_copy_helpers());
-    const size_t hbytes = q->meta + q->cap * q->stride;
-    for (auto& S : q->set) {
-        if (S.h.ensure(hbytes) || S.d.ensure(hbytes + q->cap * 21) || S.res.ensure(q->cap) ||
-            hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&S.done, hipEventDisableTiming) != hipSuccess) {
-            if (t_err.empty()) fail(SHA1CHUNK_ENOMEM, "vq: allocation failed");
-            sha1chunk_vq_destroy(q);
-            return nullptr;
-        }
-        S.tags.reserve(q->cap);
-    }
-    return q;
-}
-
-int sha1chunk_vq_submit(sha1chunk_vq* q, const void* chunk, uint32_t len, const uint8_t expected[20],
-                        uint64_t tag) {
-    if (!q || (len && !chunk) || !expected) return fail(SHA1CHUNK_EINVAL, "vq: null argument");
-    if (q->pv) {
-        if (len > q->pv->maxlen)
-            return fail(SHA1CHUNK_EINVAL, "vq: chunk of %u bytes > max %u", len, q->pv->maxlen);
-        return pvq_submit(q->pv, chunk, len, expected, tag);
-    }
+// Batch mode has no ring to reserve in: a reservation is a host buffer of
+// the queue's, committed by copying (submit) and freed on release.
+int vq_batch_submit(s1be_vq* q, const void* chunk, uint32_t len, const uint8_t expected[20], uint64_t tag) {
     if (len > q->maxlen) return fail(SHA1CHUNK_EINVAL, "vq: chunk of %u bytes > max %u", len, q->maxlen);
-    if (q->host1) {
-        uint8_t dig[20];
-        sha1host_digest(chunk, len, dig);
-        q->ready.emplace_back(tag, memcmp(dig, expected, 20) != 0 ? 1 : 0);
-        ++q->pending;
-        return SHA1CHUNK_OK;
-    }
     VqSet* S = &q->set[q->fill];
     while (S->inflight) {  // the fill set is still on the device: drain in order
         int rc = vq_collect_oldest(q);
@@ -1874,9 +1847,7 @@ int sha1chunk_vq_submit(sha1chunk_vq* q, const void* chunk, uint32_t len, const 
     return vq_maybe_launch(q);
 }
 
-int sha1chunk_vq_flush(sha1chunk_vq* q) {
-    if (!q) return fail(SHA1CHUNK_EINVAL, "vq: null queue");
-    if (q->pv) return pvq_publish(q->pv);
+int vq_batch_flush(s1be_vq* q) {
     if (q->set[q->fill].count == 0 || q->set[q->fill].inflight) return SHA1CHUNK_OK;
     int rc = vq_launch(q, q->fill);
     if (rc) return rc;
@@ -1884,12 +1855,10 @@ int sha1chunk_vq_flush(sha1chunk_vq* q) {
     return SHA1CHUNK_OK;
 }
 
-long sha1chunk_vq_poll(sha1chunk_vq* q, uint64_t* tags, uint8_t* mismatch, size_t max, int wait) {
-    if (!q || (max && (!tags || !mismatch))) return fail(SHA1CHUNK_EINVAL, "vq: null argument");
-    if (q->pv) return pvq_poll(q->pv, tags, mismatch, max, wait);
+long vq_batch_poll(s1be_vq* q, uint64_t* tags, uint8_t* mismatch, size_t max, int wait) {
     int rc;
     if (wait) {
-        if ((rc = sha1chunk_vq_flush(q))) return rc;
+        if ((rc = vq_batch_flush(q))) return rc;
         while (!q->flight.empty())
             if ((rc = vq_collect_oldest(q))) return rc;
     } else {
@@ -1907,12 +1876,139 @@ long sha1chunk_vq_poll(sha1chunk_vq* q, uint64_t* tags, uint8_t* mismatch, size_
     return static_cast<long>(n);
 }
 
-size_t sha1chunk_vq_pending(const sha1chunk_vq* q) { return q ? (q->pv ? q->pv->pending : q->pending) : 0; }
+}  // namespace
 
-void sha1chunk_vq_destroy(sha1chunk_vq* q) {
+// The backend's queue entry points take and return the queue as void*
+// (the front end's handle type); every call holds the queue's lock, so any
+// thread may reserve, fill, commit, release and poll on a shared queue.
+extern "C" {
+
+void s1be_vq_destroy(void* qv);
+
+void* s1be_vq_create(size_t batch, uint32_t max_chunk_len) {
+    if (batch == 0 || batch > (1u << 20) || max_chunk_len == 0) {
+        fail(SHA1CHUNK_EINVAL, "vq: batch 1..2^20 and max_chunk_len > 0 required");
+        return nullptr;
+    }
+    Device* D;
+    if (get_device(&D)) return nullptr;
+    auto* q = new s1be_vq();
+    q->dev = D->id;
+    // the persistent drain unless SHA1CHUNK_VQ_MODE=batch (launch per batch)
+    // or the device's drain CU budget is spent (then batch launches too)
+    const char* mode = getenv("SHA1CHUNK_VQ_MODE");
+    const int cus = mode && !strcmp(mode, "batch") ? 0 : drain_cus_take(D);
+    if (cus > 0) {
+        q->pv = pvq_create(D, batch, max_chunk_len, cus);
+        if (!q->pv) {
+            delete q;
+            return nullptr;
+        }
+        return q;
+    }
+    q->cus = D->cus;
+    q->batch = batch;
+    q->cap = vq_cap(batch);
+    q->maxlen = max_chunk_len;
+    q->stride = round_up(max_chunk_len, kAlign);
+    q->meta = round_up(q->cap * (8 + 4 + 20), kAlign);
+    q->copier = new PartPool(vq_copy_helpers());
+    const size_t hbytes = q->meta + q->cap * q->stride;
+    for (auto& S : q->set) {
+        if (S.h.ensure(hbytes) || S.d.ensure(hbytes + q->cap * 21) || S.res.ensure(q->cap) ||
+            hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&S.done, hipEventDisableTiming) != hipSuccess) {
+            if (t_err.empty()) fail(SHA1CHUNK_ENOMEM, "vq: allocation failed");
+            s1be_vq_destroy(q);
+            return nullptr;
+        }
+        S.tags.reserve(q->cap);
+    }
+    return q;
+}
+
+int s1be_vq_submit(void* qv, const void* chunk, uint32_t len, const uint8_t expected[20], uint64_t tag) {
+    auto* q = static_cast<s1be_vq*>(qv);
+    if (!q || (len && !chunk) || !expected) return fail(SHA1CHUNK_EINVAL, "vq: null argument");
+    std::lock_guard<std::mutex> lk(q->mu);
+    if (q->pv) {
+        if (len > q->pv->maxlen)
+            return fail(SHA1CHUNK_EINVAL, "vq: chunk of %u bytes > max %u", len, q->pv->maxlen);
+        return pvq_submit(q->pv, chunk, len, expected, tag);
+    }
+    return vq_batch_submit(q, chunk, len, expected, tag);
+}
+
+void* s1be_vq_reserve(void* qv, uint32_t len) {
+    auto* q = static_cast<s1be_vq*>(qv);
+    if (!q) {
+        fail(SHA1CHUNK_EINVAL, "vq: null queue");
+        return nullptr;
+    }
+    std::lock_guard<std::mutex> lk(q->mu);
+    const uint32_t maxlen = q->pv ? q->pv->maxlen : q->maxlen;
+    if (len > maxlen) {
+        fail(SHA1CHUNK_EINVAL, "vq: reservation of %u bytes > max %u", len, maxlen);
+        return nullptr;
+    }
+    if (q->pv) return pvq_reserve(q->pv, len);
+    auto buf = std::unique_ptr<uint8_t[]>(new (std::nothrow) uint8_t[std::max<uint32_t>(len, 1)]);
+    if (!buf) {
+        fail(SHA1CHUNK_ENOMEM, "vq: reservation of %u bytes", len);
+        return nullptr;
+    }
+    void* p = buf.get();
+    q->reserved.emplace(p, std::make_pair(len, std::move(buf)));
+    return p;
+}
+
+int s1be_vq_commit(void* qv, void* buf, uint32_t len, const uint8_t expected[20], uint64_t tag) {
+    auto* q = static_cast<s1be_vq*>(qv);
+    if (!q || !buf || !expected) return fail(SHA1CHUNK_EINVAL, "vq: null argument");
+    std::lock_guard<std::mutex> lk(q->mu);
+    if (q->pv) return pvq_commit(q->pv, buf, len, expected, tag);
+    auto it = q->reserved.find(buf);
+    if (it == q->reserved.end()) return fail(SHA1CHUNK_EINVAL, "vq: %p is not a reserved buffer", buf);
+    if (len > it->second.first)
+        return fail(SHA1CHUNK_EINVAL, "vq: commit of %u bytes into a %u-byte reservation", len, it->second.first);
+    return vq_batch_submit(q, buf, len, expected, tag);
+}
+
+int s1be_vq_release(void* qv, void* buf) {
+    auto* q = static_cast<s1be_vq*>(qv);
+    if (!q || !buf) return fail(SHA1CHUNK_EINVAL, "vq: null argument");
+    std::lock_guard<std::mutex> lk(q->mu);
+    if (q->pv) return pvq_release(q->pv, buf);
+    if (!q->reserved.erase(buf)) return fail(SHA1CHUNK_EINVAL, "vq: %p is not a reserved buffer", buf);
+    return SHA1CHUNK_OK;
+}
+
+int s1be_vq_flush(void* qv) {
+    auto* q = static_cast<s1be_vq*>(qv);
+    if (!q) return fail(SHA1CHUNK_EINVAL, "vq: null queue");
+    std::lock_guard<std::mutex> lk(q->mu);
+    return q->pv ? pvq_publish(q->pv) : vq_batch_flush(q);
+}
+
+long s1be_vq_poll(void* qv, uint64_t* tags, uint8_t* mismatch, size_t max, int wait) {
+    auto* q = static_cast<s1be_vq*>(qv);
+    if (!q || (max && (!tags || !mismatch))) return fail(SHA1CHUNK_EINVAL, "vq: null argument");
+    std::lock_guard<std::mutex> lk(q->mu);
+    return q->pv ? pvq_poll(q->pv, tags, mismatch, max, wait) : vq_batch_poll(q, tags, mismatch, max, wait);
+}
+
+size_t s1be_vq_pending(const void* qv) {
+    auto* q = static_cast<s1be_vq*>(const_cast<void*>(qv));
+    if (!q) return 0;
+    std::lock_guard<std::mutex> lk(q->mu);
+    return q->pv ? q->pv->pending : q->pending;
+}
+
+void s1be_vq_destroy(void* qv) {
+    auto* q = static_cast<s1be_vq*>(qv);
     if (!q) return;
-    if (q->pv || q->host1) {
-        if (q->pv) pvq_destroy(q->pv);
+    if (q->pv) {
+        pvq_destroy(q->pv);
         delete q;
         return;
     }

@@ -97,6 +97,9 @@ _SIGNATURES = [
     ("sha1chunk_synth_fill_ragged_async", C.c_int, [_vp, _vp, _vp, C.c_uint64, C.c_uint64, C.c_uint64, _vp]),
     ("sha1chunk_vq_create", C.c_void_p, [C.c_size_t, C.c_uint32]),
     ("sha1chunk_vq_submit", C.c_int, [_vp, _vp, C.c_uint32, _u8p, C.c_uint64]),
+    ("sha1chunk_vq_reserve", C.c_void_p, [_vp, C.c_uint32]),
+    ("sha1chunk_vq_commit", C.c_int, [_vp, _vp, C.c_uint32, _u8p, C.c_uint64]),
+    ("sha1chunk_vq_release", C.c_int, [_vp, _vp]),
     ("sha1chunk_vq_flush", C.c_int, [_vp]),
     ("sha1chunk_vq_poll", C.c_long, [_vp, _u64p, _u8p, C.c_size_t, C.c_int]),
     ("sha1chunk_vq_pending", C.c_size_t, [_vp]),
@@ -104,6 +107,7 @@ _SIGNATURES = [
     ("sha1chunk_device_count", C.c_int, []),
     ("sha1chunk_set_device", C.c_int, [C.c_int]),
     ("sha1chunk_get_device", C.c_int, []),
+    ("sha1chunk_device_pci_bus_id", C.c_int, [C.c_int, C.c_char_p, C.c_size_t]),
     ("sha1chunk_last_error", C.c_char_p, []),
     ("sha1chunk_version", C.c_char_p, []),
 ]
@@ -152,6 +156,13 @@ def device_count() -> int:
 
 def set_device(dev: int) -> None:
     _check(lib().sha1chunk_set_device(dev), "sha1chunk_set_device")
+
+
+def device_pci_bus_id(dev: int) -> str:
+    """PCI address of logical device `dev`'s physical GPU."""
+    buf = C.create_string_buffer(64)
+    _check(lib().sha1chunk_device_pci_bus_id(dev, buf, len(buf)), "sha1chunk_device_pci_bus_id")
+    return buf.value.decode()
 
 
 def version() -> str:
@@ -279,6 +290,16 @@ def verify_batch(base, offsets, lengths, expected: np.ndarray) -> np.ndarray:
     return mism
 
 
+class Reservation:
+    """A buffer handed out by VerifyQueue.reserve(): `view` is a writable
+    uint8 array over it (valid until the queue releases it)."""
+
+    def __init__(self, ptr: int, length: int):
+        self.ptr = ptr
+        self.length = length
+        self.view = np.ctypeslib.as_array(C.cast(ptr, _u8p), shape=(max(length, 1),))[:length]
+
+
 class VerifyQueue:
     """Asynchronous batched verify for the peer's receive path: the batched
     counterpart of verify_hash() (job.c:217-228).  submit() stages a chunk
@@ -298,6 +319,28 @@ class VerifyQueue:
         e = np.frombuffer(exp, np.uint8)
         b = bytes(chunk)
         _check(lib().sha1chunk_vq_submit(self._q, b, len(b), _np_ptr(e), tag), "sha1chunk_vq_submit")
+
+    def reserve(self, length: int) -> "Reservation":
+        """A buffer of `length` bytes inside the queue (the peer's session
+        buffer, reliable_udp.c:121): fill `.view` in place, then commit()."""
+        p = lib().sha1chunk_vq_reserve(self._q, length)
+        if not p:
+            raise Sha1ChunkError(ENOMEM, "sha1chunk_vq_reserve",
+                                 lib().sha1chunk_last_error().decode(errors="replace"))
+        return Reservation(p, length)
+
+    def commit(self, r: "Reservation", expected: bytes | str, tag: int, length: int | None = None) -> None:
+        """Verify a filled reservation where it lies (packet_handler.c:472)."""
+        exp = bytes.fromhex(expected) if isinstance(expected, str) else bytes(expected)
+        if len(exp) != DIGEST_LEN:
+            raise ValueError("expected digest must be 20 bytes / 40 hex chars")
+        e = np.frombuffer(exp, np.uint8)
+        n = r.length if length is None else length
+        _check(lib().sha1chunk_vq_commit(self._q, r.ptr, n, _np_ptr(e), tag), "sha1chunk_vq_commit")
+
+    def release(self, r: "Reservation") -> None:
+        """Give a reservation back (after its result, or instead of a commit)."""
+        _check(lib().sha1chunk_vq_release(self._q, r.ptr), "sha1chunk_vq_release")
 
     def flush(self) -> None:
         _check(lib().sha1chunk_vq_flush(self._q), "sha1chunk_vq_flush")

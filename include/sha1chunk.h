@@ -9,6 +9,12 @@
  * sha1chunk_hash_batch() replaces a loop of those calls; the reference-
  * signature functions in chunk_hash.h / sha.h are implemented on top of it.
  *
+ * The library is two files: libsha1chunk.so (what callers link: these
+ * symbols, a thin C front end on libc alone) and libsha1chunk_hip.so (the
+ * HIP runtime and gfx950 kernels), which the front end loads from its own
+ * directory on the first call that needs the GPU -- so a process whose
+ * calls all take the host small-call path below never starts HIP.
+ *
  * Error convention: 0 on success, a negative SHA1CHUNK_E* code otherwise
  * (never exit()); sha1chunk_last_error() returns a thread-local message.
  * There is no CPU fallback: without a usable gfx950 device every call
@@ -171,16 +177,36 @@ int sha1chunk_synth_fill_ragged_async(void *d_base, const uint64_t *d_offsets,
  * poll() returns the results in submission order.  A device is still
  * required.
  *
- * Both: one queue per thread; queues on one device share nothing.  The copy
- * is split over SHA1CHUNK_VQ_THREADS threads (default 4, the caller
- * included: three helper threads per queue that spin briefly between
- * submissions).  Measured on 16384 x 512 KiB host chunks: 26-35 GiB/s
+ * Every queue call takes the queue's lock, so several threads (receive
+ * sessions) may share one queue.  Persistent drains of all queues on one
+ * device hold at most SHA1CHUNK_VQ_CU_BUDGET CUs (default half the device);
+ * a queue created when that budget is spent uses batch launches.  The copy
+ * of submit() is split over SHA1CHUNK_VQ_THREADS threads (default 4, the
+ * caller included: three helper threads per queue that spin briefly between
+ * submissions); reserve/commit has no copy.  Measured on 16384 x 512 KiB host chunks: 26-35 GiB/s
  * persistent, 23-37 GiB/s batch. */
 typedef struct sha1chunk_vq sha1chunk_vq;
 /* NULL on failure (sha1chunk_last_error() says why). */
 sha1chunk_vq *sha1chunk_vq_create(size_t batch, uint32_t max_chunk_len);
 int sha1chunk_vq_submit(sha1chunk_vq *q, const void *chunk, uint32_t len,
                         const uint8_t expected[20], uint64_t tag);
+/* Zero-copy receive.  reserve() hands out a buffer of len (<= max_chunk_len)
+ * bytes inside the queue's pinned ring -- the peer's per-session receive
+ * buffer (reliable_udp.c:121 recv_session->data), filled in place as DATA
+ * packets arrive (reliable_udp.c:339) -- and commit() verifies it where it
+ * lies, with no copy (the call at packet_handler.c:472).  The buffer must
+ * not change between commit() and its result; it stays valid after the
+ * result is polled, until release() (after the caller copied the verified
+ * chunk into its job buffer, reliable_udp.c:696-709, or dropped it).  A
+ * reservation may also be released without a commit.  Unreleased buffers
+ * hold ring space: reserve() fails (NULL, SHA1CHUNK_ENOMEM) rather than
+ * wait when only the caller can free the room it needs.  In batch mode and
+ * on the batch-1 host path the buffer is ordinary host memory (commit
+ * copies it, resp. hashes it in place). */
+void *sha1chunk_vq_reserve(sha1chunk_vq *q, uint32_t len);
+int sha1chunk_vq_commit(sha1chunk_vq *q, void *buf, uint32_t len, const uint8_t expected[20],
+                        uint64_t tag);
+int sha1chunk_vq_release(sha1chunk_vq *q, void *buf);
 int sha1chunk_vq_flush(sha1chunk_vq *q);
 /* Up to max finished results; wait != 0 blocks until everything submitted so
  * far has finished.  Returns the number written (>= 0) or a negative error. */
@@ -193,6 +219,11 @@ void sha1chunk_vq_destroy(sha1chunk_vq *q);
 int sha1chunk_device_count(void);
 int sha1chunk_set_device(int device);
 int sha1chunk_get_device(void);
+/* PCI address ("dddd:bb:dd.f") of logical device `device`'s physical GPU:
+ * tells apart the devices SHA1CHUNK_ALL_DEVICES / SHA1CHUNK_FILE_DEVICES
+ * shard over (several logical devices map to one GPU only under
+ * SHA1CHUNK_VIRTUAL_DEVICES, a test knob). */
+int sha1chunk_device_pci_bus_id(int device, char *buf, size_t len);
 /* Last error text of this thread ("" if none). */
 const char *sha1chunk_last_error(void);
 /* "gfx950:<kernels>" build identity, for logs. */

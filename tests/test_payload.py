@@ -16,9 +16,11 @@ PKG = "congestion-control-with-bittorren_amd"
 # built files a GPU run loads (tests/test_gpu_*.py, __graft_entry__.smoke, bench.py)
 NEEDED = [
     f"{PKG}/libsha1chunk.so",
+    f"{PKG}/libsha1chunk_hip.so",
     f"{PKG}/make-chunks",
     f"{PKG}/build-asan/asan_driver",
     f"{PKG}/build-asan/libsha1chunk.so",
+    f"{PKG}/build-asan/libsha1chunk_hip.so",
     "oracle/liboracle.so",
     "oracle/_ref/libsharef.so",
     "oracle/_ref/dropin/make-chunks",
