@@ -61,11 +61,13 @@ struct VqDrainArgs {
     uint32_t* alive;         // host: per workgroup, 1 while it may still claim
     uint8_t* res;            // host: per slot, 0 match / 1 mismatch
     uint32_t* done;          // host: per group ring entry, group index + 1 when done
+    uint32_t* last_done;     // host: the last group finished (index + 1), any order
     uint8_t* dig;            // device: per slot, digest scratch
     uint32_t* claim;         // device: groups claimed so far
     uint32_t grp_ring;       // group ring entries
     uint32_t pad;
     uint64_t idle_ticks;     // 100 MHz ticks without work before a workgroup exits
+    uint64_t life_ticks;     // 100 MHz ticks after which a workgroup exits even under load
 };
 hipError_t launch_vq_drain(const VqDrainArgs& Q, uint32_t grid, hipStream_t st);
 

@@ -214,7 +214,17 @@ __device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) {
 // queue's, not the workgroup's: `last` is when the claim counter last moved
 // (any workgroup's claim), so under load no workgroup leaves, and after a
 // quiet spell the drain's workgroups leave together.
-__device__ uint32_t vq_next(const VqDrainArgs& Q, uint64_t& last, uint32_t& seen) {
+__device__ uint32_t vq_next(const VqDrainArgs& Q, uint64_t& last, uint32_t& seen, uint64_t born) {
+    // Bounded lifetime: a drain that never went idle would hold its hardware
+    // queue for good, and HIP serves every stream mapped onto that queue (a
+    // process has GPU_MAX_HW_QUEUES = 4 of them) in order behind it -- another
+    // queue's setup or drain, a hash batch.  Past life_ticks the workgroup
+    // leaves between groups, work pending or not; the host relaunches the
+    // drain on its next call (pvq_ensure_drain counts the live workgroups).
+    if (__builtin_amdgcn_s_memrealtime() - born > Q.life_ticks) {
+        st_sys(Q.alive + blockIdx.x, 0u);
+        return kVqExit;
+    }
     for (int round = 0; round < 2; ++round) {
         uint32_t p = ld_sys(Q.pub);
         uint32_t c = __hip_atomic_load(Q.claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -248,10 +258,11 @@ __global__ __launch_bounds__(kMixedThreads) void sha1_vq_drain_kernel(VqDrainArg
     const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     uint64_t last = __builtin_amdgcn_s_memrealtime();
+    const uint64_t born = last;
     uint32_t seen = 0xffffffffu;
     uint32_t backoff = 1;
     for (;;) {
-        if (threadIdx.x == 0) slot[0] = vq_next(Q, last, seen);
+        if (threadIdx.x == 0) slot[0] = vq_next(Q, last, seen, born);
         __syncthreads();
         const uint32_t g = __builtin_amdgcn_readfirstlane(slot[0]);
         __syncthreads();  // every wave has the command before the LDS is reused
@@ -289,7 +300,10 @@ __global__ __launch_bounds__(kMixedThreads) void sha1_vq_drain_kernel(VqDrainArg
                 Q.res[first + lane] = diff ? 1 : 0;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-            if (lane == 0) st_sys(Q.done + gi, g + 1u);
+            if (lane == 0) {
+                st_sys(Q.done + gi, g + 1u);
+                st_sys(Q.last_done, g + 1u);  // the host scans only after this word moved
+            }
         }
     }
 }

@@ -1297,9 +1297,10 @@ int vq_maybe_launch(s1be_vq* q) {
 // is collected.
 constexpr uint32_t kPvqMaxGroup = 64;
 struct PvqCtl {
-    uint32_t pub;   // groups published (host store, release)
-    uint32_t stop;  // destroy: exit once nothing is claimable
-    uint32_t pad[30];
+    uint32_t pub;        // groups published (host store, release)
+    uint32_t stop;       // destroy: exit once nothing is claimable
+    uint32_t last_done;  // drain: index + 1 of the group it finished last
+    uint32_t pad[29];
     uint32_t alive[2][1024];  // per launch slot, per workgroup
 };
 struct PvqGroup {
@@ -1322,7 +1323,7 @@ struct Pvq {
     uint64_t nbytes = 0;  // data ring bytes
     uint32_t maxlen = 0;
     uint32_t group_max = kPvqMaxGroup;
-    uint64_t idle_ticks = 0;
+    uint64_t idle_ticks = 0, life_ticks = 0;
     // pinned, uncached host memory: data ring, then the per-slot and
     // per-group arrays, then the control words
     uint8_t* hmem = nullptr;
@@ -1342,6 +1343,7 @@ struct Pvq {
     uint64_t reg_base = 0;           // id of regions.front()
     std::unordered_map<uint64_t, uint64_t> held;  // reserved regions not released: ring offset -> id
     uint64_t slot_head = 0, slot_tail = 0, byte_head = 0, byte_tail = 0;
+    uint32_t seen_done = 0;  // ctl->last_done at the last scan
     uint64_t open_slot0 = 0;
     uint32_t open_count = 0;
     uint64_t next_g = 0;
@@ -1358,6 +1360,18 @@ struct Pvq {
     size_t hbytes = 0;
     unsigned hflags = 0;
     int budget_dev = -1;  // device whose drain CU budget this queue holds (pvq_create)
+    // DMA staging (SHA1CHUNK_VQ_DMA=1): the data ring lives in ordinary
+    // pinned host memory (`hdata`), each published group's chunks are copied
+    // by the copy engine into a device mirror of the ring (`ddata`, uncached
+    // device memory, the drain reads it from HBM), and the group is released
+    // to the drain (`pub`) once its copy event has completed.
+    bool dma = false;
+    uint8_t* hdata = nullptr;
+    size_t hdata_bytes = 0;
+    uint8_t* ddata = nullptr;
+    hipStream_t cstream = nullptr;
+    std::deque<std::pair<uint64_t, hipEvent_t>> staged;  // group, its copies' event
+    std::vector<hipEvent_t> spare_events;
 };
 
 uint64_t env_u64(const char* name, uint64_t dflt) {
@@ -1365,13 +1379,13 @@ uint64_t env_u64(const char* name, uint64_t dflt) {
     return e ? strtoull(e, nullptr, 10) : dflt;
 }
 
-int pvq_launch(Pvq* P, int k) {
+int pvq_launch(Pvq* P, int k, int wgs) {
     // every workgroup of the new drain counts as alive from here on, so a
     // submit right after does not launch another one
-    for (int w = 0; w < P->cus; ++w) __atomic_store_n(&P->ctl->alive[k][w], 1u, __ATOMIC_RELEASE);
+    for (int w = 0; w < wgs; ++w) __atomic_store_n(&P->ctl->alive[k][w], 1u, __ATOMIC_RELEASE);
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
     VqDrainArgs Q{};
-    Q.data = P->data;
+    Q.data = P->dma ? P->ddata : P->data;
     Q.off = P->off;
     Q.len = P->len;
     Q.exp = P->exp;
@@ -1381,12 +1395,14 @@ int pvq_launch(Pvq* P, int k) {
     Q.alive = P->ctl->alive[k];
     Q.res = P->res;
     Q.done = P->done;
+    Q.last_done = &P->ctl->last_done;
     Q.dig = P->dmem;
     Q.claim = reinterpret_cast<uint32_t*>(P->dmem + 20ull * P->nslots);
     Q.grp_ring = P->nslots;
     Q.idle_ticks = P->idle_ticks;
+    Q.life_ticks = P->life_ticks;
     HIP_TRY(hipSetDevice(P->dev));
-    hipError_t e = launch_vq_drain(Q, static_cast<uint32_t>(P->cus), P->stream[k]);
+    hipError_t e = launch_vq_drain(Q, static_cast<uint32_t>(wgs), P->stream[k]);
     if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "vq drain launch: %s", hipGetErrorString(e));
     HIP_TRY(hipEventRecord(P->ended[k], P->stream[k]));
     P->launched[k] = true;
@@ -1394,11 +1410,14 @@ int pvq_launch(Pvq* P, int k) {
 }
 
 // After `pub` moved (and while waiting): keep the drain at full strength.
-// Workgroups leave one by one when they find nothing to claim, each with
-// the exit handshake of sha1_kernels.hip (so no published group is ever
-// left without a live workgroup that sees it).  When fewer than the drain's
-// workgroups are alive, a new drain is launched on a slot whose previous
-// drain has ended; the leftovers of the old one keep working until idle.
+// Workgroups leave when they find nothing to claim, each with the exit
+// handshake of sha1_kernels.hip (so no published group is left without a
+// live workgroup that sees it), and after their lifetime even under load
+// (SHA1CHUNK_VQ_LIFE_MS, so that no drain holds its hardware queue for
+// good); the latter relies on this call, which every submit, commit and
+// poll makes while groups are in flight.  When fewer than the drain's
+// workgroups are alive, the missing ones are launched on a slot whose
+// previous drain has ended; the leftovers of the old one keep working.
 int pvq_ensure_drain(Pvq* P) {
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
     int alive = 0;
@@ -1411,9 +1430,60 @@ int pvq_ensure_drain(Pvq* P) {
             if (q == hipErrorNotReady) continue;
             if (q != hipSuccess) return fail(SHA1CHUNK_EHIP, "vq drain: %s", hipGetErrorString(q));
         }
-        return pvq_launch(P, k);
+        return pvq_launch(P, k, P->cus - alive);
     }
     return SHA1CHUNK_OK;  // both slots' drains still leaving: the next call launches
+}
+
+// DMA staging: release every staged group whose copies have landed, in
+// order (the copy stream completes them in order), to the drain.
+int pvq_release_staged(Pvq* P) {
+    bool moved = false;
+    while (!P->staged.empty()) {
+        const hipError_t q = hipEventQuery(P->staged.front().second);
+        if (q == hipErrorNotReady) break;
+        if (q != hipSuccess) return fail(SHA1CHUNK_EHIP, "vq copy: %s", hipGetErrorString(q));
+        __atomic_store_n(&P->ctl->pub, static_cast<uint32_t>(P->staged.front().first + 1), __ATOMIC_RELEASE);
+        P->spare_events.push_back(P->staged.front().second);
+        P->staged.pop_front();
+        moved = true;
+    }
+    return moved ? pvq_ensure_drain(P) : SHA1CHUNK_OK;
+}
+
+// Copy the chunks of slots [slot0, slot0 + count) into the device ring,
+// adjacent regions in one copy, and record the group's event.
+int pvq_stage(Pvq* P, uint64_t g, uint64_t slot0, uint32_t count) {
+    HIP_TRY(hipSetDevice(P->dev));
+    uint64_t run_at = 0, run_len = 0;
+    auto flush = [&]() -> int {
+        if (run_len)
+            HIP_TRY(hipMemcpyAsync(P->ddata + run_at, P->hdata + run_at, run_len, hipMemcpyHostToDevice, P->cstream));
+        run_len = 0;
+        return SHA1CHUNK_OK;
+    };
+    for (uint32_t j = 0; j < count; ++j) {
+        const PvqRegion& r = P->regions[P->slot_reg[(slot0 + j) % P->nslots] - P->reg_base];
+        const uint64_t at = r.start % P->nbytes, len = r.end - r.start;
+        if (run_len && at == run_at + run_len) {
+            run_len += len;
+            continue;
+        }
+        if (int rc = flush()) return rc;
+        run_at = at;
+        run_len = len;
+    }
+    if (int rc = flush()) return rc;
+    hipEvent_t ev;
+    if (!P->spare_events.empty()) {
+        ev = P->spare_events.back();
+        P->spare_events.pop_back();
+    } else {
+        HIP_TRY(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    }
+    HIP_TRY(hipEventRecord(ev, P->cstream));
+    P->staged.emplace_back(g, ev);
+    return SHA1CHUNK_OK;
 }
 
 int pvq_publish(Pvq* P) {
@@ -1424,8 +1494,15 @@ int pvq_publish(Pvq* P) {
     P->grp[2 * gi + 1] = P->open_count;
     P->groups.push_back(PvqGroup{g, P->open_slot0, P->open_count, false});
     ++P->inflight;
+    const uint64_t slot0 = P->open_slot0;
+    const uint32_t count = P->open_count;
     P->open_slot0 = P->slot_tail;
     P->open_count = 0;
+    if (P->dma) {
+        // released to the drain once its copies land (pvq_release_staged)
+        if (int rc = pvq_stage(P, g, slot0, count)) return rc;
+        return pvq_release_staged(P);
+    }
     // the group's bytes, lengths, digests and descriptor are written: release them
     __atomic_store_n(&P->ctl->pub, static_cast<uint32_t>(g + 1), __ATOMIC_RELEASE);
     return pvq_ensure_drain(P);
@@ -1453,12 +1530,25 @@ void pvq_free_regions(Pvq* P) {
 // runs at most one per CU at a time, so the scan stops after 2 x CUs
 // unfinished groups in a row: a submit costs O(CUs), not O(groups in flight).
 int pvq_reap(Pvq* P) {
+    if (P->dma && !P->staged.empty())
+        if (int rc = pvq_release_staged(P)) return rc;
+    // The completion words live in uncached host memory (~0.1-0.2 us per
+    // CPU read); every submit, reserve and commit reaps, so scan them only
+    // when the drain's last-finished word moved since the last scan (each
+    // group writes its own index there, so the word changes whenever any
+    // group finished).
+    const uint32_t ld = __atomic_load_n(&P->ctl->last_done, __ATOMIC_ACQUIRE);
+    if (ld == P->seen_done) return SHA1CHUNK_OK;
+    bool whole = true;  // the scan reached the end (else scan again next time)
     size_t unfinished = 0;
     for (auto& G : P->groups) {
         if (G.collected) continue;
         const uint32_t gi = static_cast<uint32_t>(G.g % P->nslots);
         if (__atomic_load_n(&P->done[gi], __ATOMIC_ACQUIRE) != static_cast<uint32_t>(G.g + 1)) {
-            if (++unfinished > 2 * static_cast<size_t>(P->cus)) break;
+            if (++unfinished > 2 * static_cast<size_t>(P->cus)) {
+                whole = false;
+                break;
+            }
             continue;
         }
         unfinished = 0;
@@ -1475,6 +1565,7 @@ int pvq_reap(Pvq* P) {
         P->groups.pop_front();
     }
     if (P->groups.empty()) P->slot_head = P->open_slot0;
+    if (whole) P->seen_done = ld;
     pvq_free_regions(P);
     return SHA1CHUNK_OK;
 }
@@ -1565,6 +1656,40 @@ void ring_put(uint8_t* p, size_t bytes, unsigned flags) {
     (void)hipHostFree(p);  // beyond the cache: rare (more than kRingCacheMax queues destroyed at once)
 }
 
+// Device mirrors of DMA-staged rings, kept like the pinned rings (hipFree
+// can wait for the whole device).
+std::vector<std::tuple<int, uint8_t*, size_t>> g_dring_cache;
+
+uint8_t* dring_get(int dev, size_t bytes) {
+    {
+        std::lock_guard<std::mutex> lk(g_ring_mu);
+        for (size_t i = 0; i < g_dring_cache.size(); ++i)
+            if (std::get<0>(g_dring_cache[i]) == dev && std::get<2>(g_dring_cache[i]) == bytes) {
+                uint8_t* p = std::get<1>(g_dring_cache[i]);
+                g_dring_cache.erase(g_dring_cache.begin() + i);
+                return p;
+            }
+    }
+    void* p = nullptr;
+    // uncached device memory: the drain's loads go to HBM, never to an L2
+    // line left from the ring's previous lap (the copy engine does not
+    // invalidate the XCDs' L2)
+    if (hipExtMallocWithFlags(&p, bytes, hipDeviceMallocUncached) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return static_cast<uint8_t*>(p);
+}
+
+void dring_put(int dev, uint8_t* p, size_t bytes) {
+    std::lock_guard<std::mutex> lk(g_ring_mu);
+    if (g_dring_cache.size() < kRingCacheMax) {
+        g_dring_cache.emplace_back(dev, p, bytes);
+        return;
+    }
+    (void)hipFree(p);
+}
+
 // Share of the device's CUs a drain takes (SHA1CHUNK_VQ_CUS, default 64),
 // within a per-device budget for all drains (SHA1CHUNK_VQ_CU_BUDGET,
 // default half the CUs) so that queues never hold every CU: a drain
@@ -1597,10 +1722,26 @@ void pvq_destroy(Pvq* P) {
         __atomic_store_n(&P->ctl->stop, 1u, __ATOMIC_RELEASE);
         __atomic_thread_fence(__ATOMIC_SEQ_CST);
     }
-    // stream-ordered: waits for this queue's drains only, never the device
-    if (P->dmem && P->stream[0]) (void)hipFreeAsync(P->dmem, P->stream[0]);
-    for (int k = 0; k < 2; ++k) {
+    // Wait for this queue's own work only (never the whole device): both
+    // drain slots and the copy stream.  The device scratch (claim counter,
+    // digests) is freed only after both drains have ended -- a drain still
+    // running on slot 1 would otherwise write into memory the pool already
+    // handed to the next queue.
+    for (int k = 0; k < 2; ++k)
         if (P->stream[k]) (void)hipStreamSynchronize(P->stream[k]);
+    if (P->cstream) {
+        (void)hipStreamSynchronize(P->cstream);
+        (void)hipStreamDestroy(P->cstream);
+    }
+    if (P->dmem && P->stream[0]) {
+        (void)hipFreeAsync(P->dmem, P->stream[0]);
+        (void)hipStreamSynchronize(P->stream[0]);
+    }
+    for (auto& st : P->staged) (void)hipEventDestroy(st.second);
+    for (hipEvent_t ev : P->spare_events) (void)hipEventDestroy(ev);
+    if (P->hdata) ring_put(P->hdata, P->hdata_bytes, hipHostMallocDefault);
+    if (P->ddata) dring_put(P->dev, P->ddata, P->nbytes);
+    for (int k = 0; k < 2; ++k) {
         if (P->ended[k]) (void)hipEventDestroy(P->ended[k]);
         if (P->stream[k]) (void)hipStreamDestroy(P->stream[k]);
     }
@@ -1628,6 +1769,7 @@ Pvq* pvq_create(Device* D, size_t batch, uint32_t max_chunk_len, int cus) {
     P->maxlen = max_chunk_len;
     P->group_max = static_cast<uint32_t>(std::min<size_t>(batch, kPvqMaxGroup));
     P->idle_ticks = env_u64("SHA1CHUNK_VQ_IDLE_MS", 20) * 100000ull;  // s_memrealtime: 100 MHz
+    P->life_ticks = std::max<uint64_t>(1, env_u64("SHA1CHUNK_VQ_LIFE_MS", 4)) * 100000ull;
     const uint64_t stride = round_up(max_chunk_len, kAlign);
     const uint64_t ring_mib = std::max<uint64_t>(env_u64("SHA1CHUNK_VQ_RING_MIB", 1024), 1);
     P->nbytes = round_up(std::max<uint64_t>(ring_mib << 20, 2 * kPvqMaxGroup * stride), kAlign);
@@ -1636,7 +1778,12 @@ Pvq* pvq_create(Device* D, size_t batch, uint32_t max_chunk_len, int cus) {
         std::max<uint64_t>(P->nbytes / std::max<uint64_t>(kAlign, stride / 4), 4 * kPvqMaxGroup), 1u << 20));
     const size_t ns = P->nslots;
     const size_t meta = round_up(ns * 45, 4096);  // off 8, grp 8, len 4, done 4, exp 20, res 1
-    P->hbytes = P->nbytes + meta + sizeof(PvqCtl);
+    // with DMA staging the data ring is ordinary (cached) pinned memory of its
+    // own, read only by the copy engine; the slot arrays and control words
+    // stay in uncached memory the drain polls
+    P->dma = env_u64("SHA1CHUNK_VQ_DMA", 0) != 0;
+    const size_t inline_data = P->dma ? 0 : P->nbytes;
+    P->hbytes = inline_data + meta + sizeof(PvqCtl);
     P->hflags = ring_flags();
     if (!(P->hmem = ring_get(P->hbytes, P->hflags)) &&
         (P->hflags == hipHostMallocCoherent ||
@@ -1645,16 +1792,26 @@ Pvq* pvq_create(Device* D, size_t batch, uint32_t max_chunk_len, int cus) {
         pvq_destroy(P);
         return nullptr;
     }
-    memset(P->hmem + P->nbytes, 0, meta + sizeof(PvqCtl));
-    uint8_t* m = P->hmem + P->nbytes;
-    P->data = P->hmem;
+    if (P->dma) {
+        P->hdata_bytes = P->nbytes;
+        if (!(P->hdata = ring_get(P->nbytes, hipHostMallocDefault)) || !(P->ddata = dring_get(P->dev, P->nbytes)) ||
+            hipStreamCreateWithFlags(&P->cstream, hipStreamNonBlocking) != hipSuccess) {
+            (void)hipGetLastError();
+            fail(SHA1CHUNK_ENOMEM, "vq: DMA-staged ring of %llu bytes", static_cast<unsigned long long>(P->nbytes));
+            pvq_destroy(P);
+            return nullptr;
+        }
+    }
+    memset(P->hmem + inline_data, 0, meta + sizeof(PvqCtl));
+    uint8_t* m = P->hmem + inline_data;
+    P->data = P->dma ? P->hdata : P->hmem;
     P->off = reinterpret_cast<uint64_t*>(m);
     P->grp = reinterpret_cast<uint32_t*>(m + ns * 8);
     P->len = reinterpret_cast<uint32_t*>(m + ns * 16);
     P->done = reinterpret_cast<uint32_t*>(m + ns * 20);
     P->exp = m + ns * 24;
     P->res = m + ns * 44;
-    P->ctl = reinterpret_cast<PvqCtl*>(P->hmem + P->nbytes + meta);
+    P->ctl = reinterpret_cast<PvqCtl*>(P->hmem + inline_data + meta);
     P->tags.assign(ns, 0);
     P->slot_reg.assign(ns, 0);
     // streams first: the device scratch is allocated and cleared in stream

@@ -28,7 +28,7 @@ ASM = sys.argv[1] if len(sys.argv) > 1 else \
 HALF_RATE = {"v_alignbit_b32", "v_add3_u32", "v_perm_b32", "v_bfi_b32", "v_lshl_add_u32",
              "v_alignbyte_b32", "v_lshl_or_b32", "v_and_or_b32", "v_xad_u32"}
 KERNELS = {
-    "fused": "_Z17sha1_fused_kernelILi0EEv9BatchArgs",
+    "fused": "_Z17sha1_fused_kernel9BatchArgs",
     # <= 1 group of 64 chunks per CU: 4-block units, two producers
     "split_u4_2prod": "_Z17sha1_split_kernelILi4ELi1ELi8269ELi2EEv9BatchArgs",
     # <= 2 groups per CU: 8-wave workgroup, 2-block units (split_unit case 11)

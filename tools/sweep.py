@@ -55,9 +55,6 @@ def main():
                 if k.startswith("split") and k[5:].isdigit():  # split<U>: force the unit size
                     os.environ["SHA1CHUNK_SPLIT_UNIT"] = k[5:]
                     name = "split"
-                if k.startswith("fused") and k[5:].isdigit():  # fused<RV>: round-sum form (A/B lib)
-                    os.environ["SHA1CHUNK_FUSED_VARIANT"] = k[5:]
-                    name = "fused"
                 evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                        for _ in range(max(1, a.burst))]
                 for e0, e1 in evs:
@@ -66,7 +63,6 @@ def main():
                     e1.record()
                 torch.cuda.synchronize()
                 os.environ.pop("SHA1CHUNK_SPLIT_UNIT", None)
-                os.environ.pop("SHA1CHUNK_FUSED_VARIANT", None)
                 timed = evs[len(evs) // 2:]
                 times[k].append(float(np.mean([e0.elapsed_time(e1) for e0, e1 in timed])))
                 d = dig.cpu().numpy()
