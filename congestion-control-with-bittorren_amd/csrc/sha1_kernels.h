@@ -78,9 +78,14 @@ hipError_t launch_compare(const uint8_t* dig, const uint8_t* exp, uint32_t n, ui
 
 // Longest-first order of a ragged batch (sha1_sort.hip): *d_order receives n
 // indices sorted by d_len descending, *d_sorted_len the lengths in that
-// order and *d_plan 16 spare bytes of the same allocation (for the mixed
-// kernel's plan); release *scratch with hipFreeAsync on the same stream
-// after the consuming kernel has been enqueued.
+// order and *d_plan the mixed kernel's plan area of the same allocation
+// (mixed_plan_bytes(n): 256 bytes of plan words, then the planner's layout
+// summary); release *scratch with hipFreeAsync on the same stream after the
+// consuming kernel has been enqueued.
+inline size_t mixed_plan_bytes(uint32_t n) {
+    const size_t words = ((size_t(n) + 63) / 64 + 31) / 32;  // one per 32 groups of 64 chunks
+    return 256 + ((words * 12 + 255) & ~size_t(255));
+}
 hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t** d_order,
                                const uint32_t** d_sorted_len, uint32_t** d_plan, void** scratch,
                                hipStream_t st);

@@ -49,6 +49,15 @@
 
 #include "sha1_split.hpp"
 
+// The mixed planner's measured constants (us per block of a group of 64
+// chunks, see `Makespan model` below).
+#define PLAN_SPLIT4 0.743
+#define PLAN_SPLIT8 0.860
+#define PLAN_FUSED4T 1.254
+#define PLAN_FUSED4S 1.408
+#define PLAN_FUSED8T 2.502
+#define PLAN_FUSED8S 2.661
+
 // ---------------------------------------------------------------- lane ----
 __global__ __launch_bounds__(256) void sha1_lane_kernel(BatchArgs A) {
     const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -100,8 +109,10 @@ __global__ __launch_bounds__(256) void sha1_fused_kernel(BatchArgs A) {
 // 65536 x 512 KiB with permuted offsets hashed in 29.2 ms lane-per-chunk
 // against 10.4 in place.  Every shape here loads scattered chunks 8 or 16 per
 // instruction (see `shared loads`): permuted, the fused tail takes 10.8 ms
-// and the one-group split shape 24.3 as in place, so the planner ignores
-// layout (profiles/mixed_r02.json, profiles/coop_split_ab_r02.json).
+// and the one-group split shape 24.3 as in place (profiles/mixed_r02.json,
+// profiles/coop_split_ab_r02.json).  A fused wave whose chunks lie together
+// still streams lane-per-chunk, which is faster, so the planner prices the
+// fused jobs by layout (round 4: plan_layout_kernel, PLAN_FUSED*T/S).
 constexpr int kMixedThreads = 512;
 
 __global__ __launch_bounds__(kMixedThreads) void sha1_mixed_kernel(BatchArgs A) {
@@ -309,16 +320,22 @@ __global__ __launch_bounds__(kMixedThreads) void sha1_vq_drain_kernel(VqDrainArg
 }
 
 // Makespan model of a sorted ragged batch, microseconds per 64-byte block of
-// a group of 64 chunks, measured on MI355X:
+// a group of 64 chunks, measured on MI355X with one job of the shape on
+// every CU (the clock the chip holds under that load; tools/mixed_constants.sh,
+// profiles/mixed_const_r04.jsonl):
 //   chain: time of one group's block when it runs in that shape
 //   cu:    CU-time per group-block (the CU's throughput in that shape)
-// one-group split: config 2, 6.08 ms / 8193 blocks, one group per CU.
-// fused F = 4 (one wave per SIMD): 65536 x 512 KiB, 10.5 ms; F = 8 (two):
-// 131072 x 512 KiB, 19.9 ms.  8-wave split: 32768 x 512 KiB, 6.55 ms.
-constexpr double kChainSplit4 = 0.742, kCuSplit4 = 0.742;
-constexpr double kChainFused4 = 1.28, kCuFused4 = 0.320;
-constexpr double kChainFused8 = 2.43, kCuFused8 = 0.304;
-constexpr double kChainSplit8 = 0.80, kCuSplit8 = 0.40;
+// The fused shapes stream a group lane-per-chunk when its chunks lie
+// together and share each load across the wave when they lie scattered
+// (fused_coop_body), which costs a few per cent more: two constants each.
+constexpr double kChainSplit4 = PLAN_SPLIT4, kCuSplit4 = PLAN_SPLIT4;
+constexpr double kChainFused4T = PLAN_FUSED4T, kChainFused4S = PLAN_FUSED4S;
+constexpr double kChainFused8T = PLAN_FUSED8T, kChainFused8S = PLAN_FUSED8S;
+constexpr double kChainSplit8 = PLAN_SPLIT8, kCuSplit8 = PLAN_SPLIT8 / 2;
+
+__device__ __forceinline__ double fused_chain(uint32_t F, bool together) {
+    return F == 4 ? (together ? kChainFused4T : kChainFused4S) : (together ? kChainFused8T : kChainFused8S);
+}
 
 __device__ __forceinline__ uint32_t group_blocks(const uint32_t* sorted_len, uint32_t g) {
     return total_blocks(sorted_len[64ull * g]);  // a group's first lane is its longest
@@ -334,11 +351,80 @@ __device__ __forceinline__ uint32_t plan_blocks(const uint32_t* sorted_len, cons
     return g < kSimMaxG ? blocks[g] : group_blocks(sorted_len, g);
 }
 
-__device__ __forceinline__ double job_time(const uint32_t* sorted_len, const uint32_t* blocks, uint32_t mode,
-                                           uint32_t H, uint32_t F, uint32_t i) {
+// Whether group g's chunks lie together: the rule fused_coop_body applies
+// per wave (address span <= 2 x their bytes + 2 MiB).  A wave per group,
+// a lane per chunk, all groups in parallel over the chip (the planner's
+// single workgroup walking 64 dependent entries per group cost it up to
+// ~0.5 ms at 262144 chunks).  Workgroup w summarises groups 32w .. 32w+31:
+// bits[w] (bit i: group 32w+i lies together) and tb[w] (the blocks of those
+// groups, the planner's together share).
+constexpr int kLayoutThreads = 256;
+constexpr uint32_t kLayoutGroupsPerWave = 32 / (kLayoutThreads / 64);
+
+__global__ __launch_bounds__(kLayoutThreads) void plan_layout_kernel(BatchArgs A, const uint32_t* sorted_len,
+                                                                     uint64_t* tb, uint32_t* bits) {
+    const uint32_t lane = threadIdx.x % 64u, wave = threadIdx.x / 64u;
+    const uint32_t G = (A.n + 63u) / 64u;
+    __shared__ uint32_t tog[32], blk[32];
+    for (uint32_t k = 0; k < kLayoutGroupsPerWave; ++k) {
+        const uint32_t slot = wave * kLayoutGroupsPerWave + k;
+        const uint32_t g = 32u * blockIdx.x + slot;
+        if (g >= G) {  // wave-uniform
+            if (lane == 0) tog[slot] = blk[slot] = 0u;
+            continue;
+        }
+        const uint32_t e = 64u * g + lane;
+        uint64_t lo = ~0ull, hi = 0, bytes = 0;
+        if (e < A.n) {
+            const Entry en = fetch_entry(A, e);
+            lo = reinterpret_cast<uint64_t>(en.p);
+            hi = lo + en.len;
+            bytes = en.len;
+        }
+#pragma unroll
+        for (uint32_t m = 1; m < 64; m *= 2) {
+            lo = min(lo, (uint64_t)__shfl_xor((unsigned long long)lo, m));
+            hi = max(hi, (uint64_t)__shfl_xor((unsigned long long)hi, m));
+            bytes += (uint64_t)__shfl_xor((unsigned long long)bytes, m);
+        }
+        if (lane == 0) {
+            tog[slot] = hi - lo <= 2 * bytes + (2ull << 20) ? 1u : 0u;
+            blk[slot] = group_blocks(sorted_len, g);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t w = 0;
+        uint64_t b = 0;
+        for (uint32_t i = 0; i < 32; ++i) {
+            w |= tog[i] << i;
+            b += tog[i] ? blk[i] : 0u;
+        }
+        bits[blockIdx.x] = w;
+        tb[blockIdx.x] = b;
+    }
+}
+
+// The planner's layout knowledge: one bit per group < kSimMaxG (in LDS), and
+// for the groups beyond, whether most blocks lie together.
+struct PlanLayout {
+    const uint32_t* bits;
+    bool rest;
+    __device__ bool together(uint32_t g) const { return g < kSimMaxG ? ((bits[g >> 5] >> (g & 31u)) & 1u) : rest; }
+    // a fused job of F groups from g streams lane-per-chunk if all of them do
+    __device__ bool job_together(uint32_t g, uint32_t F, uint32_t G) const {
+        for (uint32_t i = g; i < min(g + F, G); ++i)
+            if (!together(i)) return false;
+        return true;
+    }
+};
+
+__device__ __forceinline__ double job_time(const uint32_t* sorted_len, const uint32_t* blocks, const PlanLayout& L,
+                                           uint32_t G, uint32_t mode, uint32_t H, uint32_t F, uint32_t i) {
     if (mode == 1) return plan_blocks(sorted_len, blocks, 2u * i) * kChainSplit8;
     if (i < H) return plan_blocks(sorted_len, blocks, i) * kChainSplit4;
-    return plan_blocks(sorted_len, blocks, H + (i - H) * F) * (F == 4 ? kChainFused4 : kChainFused8);
+    const uint32_t g = H + (i - H) * F;
+    return plan_blocks(sorted_len, blocks, g) * fused_chain(F, L.job_together(g, F, G));
 }
 
 // Estimated makespan of a plan: the largest of
@@ -348,22 +434,25 @@ __device__ __forceinline__ double job_time(const uint32_t* sorted_len, const uin
 //                                 of them back to back (rounds bound; exact
 //                                 for equal lengths)
 // where W = cu_split4 * P_H + cu_fusedF * (P_G - P_H) in mode 0 and
-// cu_split8 * P_G in mode 1 (P_H: blocks of groups 0 .. H-1).
-__device__ double makespan(const uint32_t* sorted_len, const uint32_t* blocks, uint32_t G, uint32_t C,
-                           uint32_t mode, uint32_t H, uint32_t F, uint64_t PH, uint64_t PG) {
+// cu_split8 * P_G in mode 1 (P_H: blocks of groups 0 .. H-1; cu_fusedF the
+// together / scattered constants weighted by the batch's share `ft` of
+// blocks in groups whose chunks lie together).
+__device__ double makespan(const uint32_t* sorted_len, const uint32_t* blocks, const PlanLayout& L, double ft,
+                           uint32_t G, uint32_t C, uint32_t mode, uint32_t H, uint32_t F, uint64_t PH, uint64_t PG) {
     double W;
     uint32_t J;
     if (mode == 1) {
         W = kCuSplit8 * (double)PG;
         J = (G + 1u) / 2u;
     } else {
-        W = kCuSplit4 * (double)PH + (F == 4 ? kCuFused4 : kCuFused8) * (double)(PG - PH);
+        const double cu = (ft * fused_chain(F, true) + (1.0 - ft) * fused_chain(F, false)) / F;
+        W = kCuSplit4 * (double)PH + cu * (double)(PG - PH);
         J = H + (G - H + F - 1u) / F;
     }
-    double m = fmax(W / C, job_time(sorted_len, blocks, mode, H, F, 0));
-    if (mode == 0 && H > 0 && H < G) m = fmax(m, job_time(sorted_len, blocks, mode, H, F, H));
+    double m = fmax(W / C, job_time(sorted_len, blocks, L, G, mode, H, F, 0));
+    if (mode == 0 && H > 0 && H < G) m = fmax(m, job_time(sorted_len, blocks, L, G, mode, H, F, H));
     for (uint32_t k = 1; (uint64_t)k * C < J; ++k)
-        m = fmax(m, (k + 1) * job_time(sorted_len, blocks, mode, H, F, k * C));
+        m = fmax(m, (k + 1) * job_time(sorted_len, blocks, L, G, mode, H, F, k * C));
     return m;
 }
 
@@ -379,32 +468,35 @@ __device__ double makespan(const uint32_t* sorted_len, const uint32_t* blocks, u
 // bounds already exceed the simulated time of the bounds' best plan are not
 // simulated.
 constexpr uint32_t kSimXcds = 8, kSimCus = 32;      // CUs per XCD the lane tracks at most
-constexpr float kChainSplit4f = 0.742f, kChainFused4f = 1.28f, kChainFused8f = 2.43f,
-                kChainSplit8f = 0.80f;
+constexpr float kChainSplit4f = (float)kChainSplit4, kChainSplit8f = (float)kChainSplit8;
+constexpr float kChainFused4Tf = (float)kChainFused4T, kChainFused4Sf = (float)kChainFused4S,
+                kChainFused8Tf = (float)kChainFused8T, kChainFused8Sf = (float)kChainFused8S;
 
 __device__ __forceinline__ uint32_t plan_jobs(uint32_t G, uint32_t mode, uint32_t H, uint32_t F) {
     return mode == 1 ? (G + 1u) / 2u : H + (G - H + F - 1u) / F;
 }
 
-__device__ __forceinline__ float sim_job(const uint32_t* blocks, uint32_t mode, uint32_t H, uint32_t F,
-                                         uint32_t j) {
+__device__ __forceinline__ float sim_job(const uint32_t* blocks, const PlanLayout& L, uint32_t G, uint32_t mode,
+                                         uint32_t H, uint32_t F, uint32_t j) {
     if (mode == 1) return (float)blocks[2u * j] * kChainSplit8f;
     if (j < H) return (float)blocks[j] * kChainSplit4f;
-    return (float)blocks[H + (j - H) * F] * (F == 4 ? kChainFused4f : kChainFused8f);
+    const uint32_t g = H + (j - H) * F;
+    const bool t = L.job_together(g, F, G);
+    return (float)blocks[g] * (F == 4 ? (t ? kChainFused4Tf : kChainFused4Sf) : (t ? kChainFused8Tf : kChainFused8Sf));
 }
 
 // Jobs x, x + 8, .. of a plan on one XCD's `per` CUs: the time its last CU
 // frees.  t holds the free times in ascending order (+inf past `per`); a
 // job starts at t[0] and its end is inserted in order.
-__device__ float sim_xcd(const uint32_t* blocks, uint32_t G, uint32_t mode, uint32_t H, uint32_t F,
-                         uint32_t x, uint32_t per) {
+__device__ float sim_xcd(const uint32_t* blocks, const PlanLayout& L, uint32_t G, uint32_t mode, uint32_t H,
+                         uint32_t F, uint32_t x, uint32_t per) {
     float t[kSimCus];
 #pragma unroll
     for (uint32_t i = 0; i < kSimCus; ++i) t[i] = i < per ? 0.0f : __builtin_inff();
     const uint32_t J = plan_jobs(G, mode, H, F);
 #pragma unroll 4
     for (uint32_t j = x; j < J; j += kSimXcds) {
-        const float nx = t[0] + sim_job(blocks, mode, H, F, j);
+        const float nx = t[0] + sim_job(blocks, L, G, mode, H, F, j);
         // t ascending: the new t[i] is nx clamped to [t[i], t[i+1]]
 #pragma unroll
         for (uint32_t i = 0; i + 1 < kSimCus; ++i) t[i] = __builtin_amdgcn_fmed3f(t[i], nx, t[i + 1]);
@@ -422,16 +514,19 @@ __device__ float sim_xcd(const uint32_t* blocks, uint32_t G, uint32_t mode, uint
 // (ties: smaller H).  Simulation (up to kSimMaxG groups on 8 XCDs of <= 32
 // CUs): ~80 candidates around it are simulated and the shortest wins, or
 // all-split within 0.5 % of it; beyond that, the bounds' plan or mode 1 by
-// the same bounds.  The plan depends on the lengths alone: with shared
-// loads where the chunks lie no longer changes the choice (see the
-// kernel's comment).  forced: write {fmode, fh, ff} as given (tests, A/B).
+// the same bounds.  The plan depends on the lengths and, through the fused
+// shapes' two constants, on whether each group's chunks lie together
+// (round 4: laid out longest-first, the fused tail streams lane-per-chunk
+// and a split head + fused tail beats the 8-wave mode).  forced: write
+// {fmode, fh, ff} as given (tests, A/B).
 constexpr int kPlanThreads = 1024;
 constexpr uint32_t kPlanMaxH = 4096;  // largest split head the model search considers
 
 __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, const uint32_t* sorted_len,
                                                                   uint32_t cus, uint32_t hcap, int forced,
                                                                   uint32_t fmode, uint32_t fh, uint32_t ff,
-                                                                  uint32_t* plan) {
+                                                                  uint32_t* plan, const uint64_t* lay_tb,
+                                                                  const uint32_t* lay_bits) {
     const uint32_t n = A.n;
     const uint32_t t = threadIdx.x;
     if (t == 0) plan[3] = 0u;  // the persistent kernel's job counter
@@ -450,14 +545,24 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     const uint32_t G = (n + 63u) / 64u;
     const uint32_t per = (G + kPlanThreads - 1) / kPlanThreads;
     const uint32_t g0 = min(G, t * per), g1 = min(G, g0 + per);
-    uint64_t local = 0;
+    uint64_t local = 0, local_t = 0;
     __shared__ uint32_t blocks[kSimMaxG];  // group_blocks of groups < kSimMaxG, for the simulation
+    __shared__ uint32_t togw[kSimMaxG / 32];  // plan_layout_kernel's bits, groups < kSimMaxG
+    __shared__ uint64_t tog_blocks;
+    if (t == 0) tog_blocks = 0;
     for (uint32_t g = g0; g < g1; ++g) {
         const uint32_t b = group_blocks(sorted_len, g);
         if (g < kSimMaxG) blocks[g] = b;
         local += b;
     }
+    const uint32_t W = (G + 31u) / 32u;
+    for (uint32_t w = t; w < W; w += kPlanThreads) {
+        if (w < kSimMaxG / 32) togw[w] = lay_bits[w];
+        local_t += lay_tb[w];
+    }
+    __syncthreads();
     scan[t] = local;
+    atomicAdd(reinterpret_cast<unsigned long long*>(&tog_blocks), static_cast<unsigned long long>(local_t));
     __syncthreads();
     for (uint32_t off = 1; off < kPlanThreads; off <<= 1) {
         const uint64_t v = t >= off ? scan[t - off] : 0ull;
@@ -466,6 +571,8 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         __syncthreads();
     }
     const uint64_t PG = scan[kPlanThreads - 1];
+    const double ft = PG ? (double)tog_blocks / (double)PG : 1.0;
+    const PlanLayout L{togw, ft >= 0.5};
     // P_H for every candidate H <= hcap, then each thread takes H = t, t + 1024, ..
     uint64_t P = scan[t] - local;  // P_{g0}
     for (uint32_t g = g0; g <= g1 && g <= hcap; ++g) {
@@ -477,12 +584,12 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     uint32_t bh = 0, bf = 4;
     for (uint32_t H = t; H <= hcap; H += kPlanThreads) {
         for (uint32_t F = 4; F <= (H < G ? 8u : 4u); F += 4) {  // H = G: every group split
-            const double m = makespan(sorted_len, blocks, G, cus, 0, H, F, prefix[H], PG);
+            const double m = makespan(sorted_len, blocks, L, ft, G, cus, 0, H, F, prefix[H], PG);
             if (m < bm) { bm = m; bh = H; bf = F; }
         }
     }
     if (t == 0 && G > hcap) {  // H = G beyond the searched head sizes
-        const double m = makespan(sorted_len, blocks, G, cus, 0, G, 4, PG, PG);
+        const double m = makespan(sorted_len, blocks, L, ft, G, cus, 0, G, 4, PG, PG);
         if (m < bm) { bm = m; bh = G; bf = 4; }
     }
     best_m[t] = bm;
@@ -504,7 +611,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     const bool simulate = G <= kSimMaxG && cus % kSimXcds == 0 && cus / kSimXcds <= kSimCus;
     if (!simulate) {
         if (t == 0) {
-            const bool split8 = makespan(sorted_len, blocks, G, cus, 1, 0, 0, 0, PG) < best_m[0];
+            const bool split8 = makespan(sorted_len, blocks, L, ft, G, cus, 1, 0, 0, 0, PG) < best_m[0];
             plan[0] = split8 ? 1u : 0u;
             plan[1] = split8 ? 0u : best_h[0];
             plan[2] = split8 ? 0u : best_f[0];
@@ -552,12 +659,12 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         bool run = pass == 0 ? c == 0 : (c >= 1 && c < ncand);
         if (run && pass == 1) {
             const uint32_t m = cmode[c], h = chead[c], f = cf[c];
-            const double lb = m == 1 ? makespan(sorted_len, blocks, G, cus, 1, 0, 0, 0, PG)
-                                     : makespan(sorted_len, blocks, G, cus, 0, h, f, h <= hcap ? prefix[h] : PG, PG);
+            const double lb = m == 1 ? makespan(sorted_len, blocks, L, ft, G, cus, 1, 0, 0, 0, PG)
+                                     : makespan(sorted_len, blocks, L, ft, G, cus, 0, h, f, h <= hcap ? prefix[h] : PG, PG);
             run = lb < (double)cmk[0];
         }
         float mk = __builtin_inff();
-        if (run) mk = sim_xcd(blocks, G, cmode[c], chead[c], cf[c], x, cus / kSimXcds);
+        if (run) mk = sim_xcd(blocks, L, G, cmode[c], chead[c], cf[c], x, cus / kSimXcds);
 #pragma unroll
         for (uint32_t m = 1; m < kSimXcds; m *= 2) mk = fmaxf(mk, __shfl_xor(mk, m));
         if (x == 0 && (pass == 0 ? c == 0 : c >= 1)) cmk[c] = mk;
@@ -682,9 +789,16 @@ hipError_t launch_mixed(const BatchArgs& A, const uint32_t* sorted_len, uint32_t
     const uint32_t groups = (A.n + 63u) / 64u;
     uint32_t hcap;
     const uint32_t grid = mixed_grid(groups, cus, &hcap);
+    // plan area (mixed_plan_bytes): 64 plan words, then the layout summary
+    const uint32_t words = (groups + 31u) / 32u;
+    uint64_t* lay_tb = reinterpret_cast<uint64_t*>(plan + 64);
+    uint32_t* lay_bits = reinterpret_cast<uint32_t*>(lay_tb + words);
+    if (!forced) hipLaunchKernelGGL(plan_layout_kernel, dim3(words), dim3(kLayoutThreads), 0, st, A, sorted_len,
+                                    lay_tb, lay_bits);
     hipLaunchKernelGGL(plan_mixed_kernel, dim3(1), dim3(kPlanThreads), 0, st, A, sorted_len,
                        (uint32_t)cus, hcap, forced ? 1 : 0, forced ? (uint32_t)forced[0] : 0u,
-                       forced ? (uint32_t)forced[1] : 0u, forced ? (uint32_t)forced[2] : 0u, plan);
+                       forced ? (uint32_t)forced[1] : 0u, forced ? (uint32_t)forced[2] : 0u, plan, lay_tb,
+                       lay_bits);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     BatchArgs B = A;

@@ -21,6 +21,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <emmintrin.h>
 #include <functional>
 #include <memory>
 #include <mutex>
@@ -1344,6 +1345,8 @@ struct Pvq {
     std::unordered_map<uint64_t, uint64_t> held;  // reserved regions not released: ring offset -> id
     uint64_t slot_head = 0, slot_tail = 0, byte_head = 0, byte_tail = 0;
     uint32_t seen_done = 0;  // ctl->last_done at the last scan
+    int64_t alive_scan_ns = 0;  // pvq_ensure_drain: when it last read the alive words
+    int alive_seen = 0;         // and how many it found (or launched)
     uint64_t open_slot0 = 0;
     uint32_t open_count = 0;
     uint64_t next_g = 0;
@@ -1418,11 +1421,38 @@ int pvq_launch(Pvq* P, int k, int wgs) {
 // poll makes while groups are in flight.  When fewer than the drain's
 // workgroups are alive, the missing ones are launched on a slot whose
 // previous drain has ended; the leftovers of the old one keep working.
+//
+// The alive words are uncached host memory (a CPU read costs ~0.15 us, and
+// every submit, commit and poll lands here under the queue's lock), so they
+// are read 16 bytes at a time, and not again within kAliveScanNs of a scan
+// that found the drain at full strength: a workgroup that leaves in that
+// window is replaced at most that much later (workgroups live >= 4 ms).
+constexpr int64_t kAliveScanNs = 50000;
+
+int64_t mono_ns() {
+    timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return int64_t(ts.tv_sec) * 1000000000 + ts.tv_nsec;
+}
+
+int count_alive(const uint32_t* a, int n) {
+    int c = 0, w = 0;
+    for (; w + 4 <= n; w += 4) {  // one 16-byte uncached read per 4 words
+        const __m128i v = _mm_load_si128(reinterpret_cast<const __m128i*>(a + w));
+        c += 4 - __builtin_popcount(_mm_movemask_ps(_mm_castsi128_ps(_mm_cmpeq_epi32(v, _mm_setzero_si128()))));
+    }
+    for (; w < n; ++w) c += __atomic_load_n(a + w, __ATOMIC_ACQUIRE) != 0;
+    return c;
+}
+
 int pvq_ensure_drain(Pvq* P) {
+    const int64_t now = mono_ns();
+    if (P->alive_seen >= P->cus && now - P->alive_scan_ns < kAliveScanNs) return SHA1CHUNK_OK;
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
-    int alive = 0;
-    for (int k = 0; k < 2; ++k)
-        for (int w = 0; w < P->cus; ++w) alive += __atomic_load_n(&P->ctl->alive[k][w], __ATOMIC_ACQUIRE) != 0;
+    const int alive = count_alive(P->ctl->alive[0], P->cus) + count_alive(P->ctl->alive[1], P->cus);
+    __atomic_thread_fence(__ATOMIC_ACQUIRE);
+    P->alive_scan_ns = now;
+    P->alive_seen = alive;
     if (alive >= P->cus) return SHA1CHUNK_OK;
     for (int k = 0; k < 2; ++k) {
         if (P->launched[k]) {
@@ -1430,6 +1460,7 @@ int pvq_ensure_drain(Pvq* P) {
             if (q == hipErrorNotReady) continue;
             if (q != hipSuccess) return fail(SHA1CHUNK_EHIP, "vq drain: %s", hipGetErrorString(q));
         }
+        P->alive_seen = P->cus;  // pvq_launch marks the new workgroups alive
         return pvq_launch(P, k, P->cus - alive);
     }
     return SHA1CHUNK_OK;  // both slots' drains still leaving: the next call launches

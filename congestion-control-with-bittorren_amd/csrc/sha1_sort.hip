@@ -33,13 +33,14 @@ hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t
     if (e != hipSuccess) return e;
     const size_t arr = align256(size_t(n) * sizeof(uint32_t));
     void* base = nullptr;
-    e = hipMallocAsync(&base, 2 * arr + 256 + align256(temp_bytes), st);
+    const size_t planb = mixed_plan_bytes(n);
+    e = hipMallocAsync(&base, 2 * arr + planb + align256(temp_bytes), st);
     if (e != hipSuccess) return e;
     uint8_t* b = static_cast<uint8_t*>(base);
     uint32_t* keys_out = reinterpret_cast<uint32_t*>(b);
     uint32_t* vals_out = reinterpret_cast<uint32_t*>(b + arr);
     uint32_t* plan = reinterpret_cast<uint32_t*>(b + 2 * arr);
-    void* temp = b + 2 * arr + 256;
+    void* temp = b + 2 * arr + planb;
     e = rocprim::radix_sort_pairs_desc(temp, temp_bytes, d_len, keys_out, ids, vals_out, n, 0, 32, st);
     if (e != hipSuccess) {
         (void)hipFreeAsync(base, st);

@@ -15,10 +15,21 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-# plan_mixed_kernel's model (us per block of a group of 64 chunks)
-CHAIN = {"split4": 0.742, "fused4": 1.28, "fused8": 2.43, "split8": 0.80}
-CU = {"split4": 0.742, "fused4": 0.320, "fused8": 0.304, "split8": 0.40}
+# plan_mixed_kernel's model (us per block of a group of 64 chunks; the
+# fused shapes with the group's chunks together "T" or scattered "S"),
+# parsed from the kernel source so the restatement cannot drift from it
+def _plan_constants():
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "congestion-control-with-bittorren_amd", "csrc", "sha1_kernels.hip")).read()
+    return {k.lower(): float(v) for k, v in re.findall(r"#define PLAN_(\w+) ([0-9.]+)", src)}
+
+
+_K = _plan_constants()
+CHAIN = {"split4": _K["split4"], "split8": _K["split8"], "fused4T": _K["fused4t"], "fused4S": _K["fused4s"],
+         "fused8T": _K["fused8t"], "fused8S": _K["fused8s"]}
+CU = {"split4": CHAIN["split4"], "split8": CHAIN["split8"] / 2}
 PLAN_MAX_H = 4096
+TOGETHER_SLACK = 2 << 20  # fused_coop_body: span <= 2 x bytes + 2 MiB
 
 
 @pytest.fixture(scope="module")
@@ -44,17 +55,43 @@ def grid_of(G, C):
     return min(G, 4 * C, PLAN_MAX_H), G
 
 
-def model_makespan(B, C, mode, H, F, P):
+def fused_chain(F, together):
+    return CHAIN[f"fused{F}{'T' if together else 'S'}"]
+
+
+class Layout:
+    """plan_mixed_kernel's PlanLayout: a together bit per sorted group below
+    SIM_MAX_G, the majority answer beyond, and the together share of blocks."""
+
+    def __init__(self, tog, B):
+        self.tog = [bool(x) for x in tog]
+        PG = sum(B)
+        self.ft = (sum(b for b, t in zip(B, self.tog) if t) / PG) if PG else 1.0
+        self.rest = self.ft >= 0.5
+
+    def together(self, g):
+        return self.tog[g] if g < SIM_MAX_G else self.rest
+
+    def job_together(self, g, F, G):
+        return all(self.together(i) for i in range(g, min(g + F, G)))
+
+
+def model_makespan(B, C, mode, H, F, P, L):
     """plan_mixed_kernel's `makespan`, restated."""
     G = len(B)
     if mode == 1:
         W, J = CU["split8"] * P[G], (G + 1) // 2
         job = lambda i: B[2 * i] * CHAIN["split8"]
     else:
-        fk = f"fused{F}"
-        W = CU["split4"] * P[H] + CU[fk] * (P[G] - P[H])
+        cu = (L.ft * fused_chain(F, True) + (1.0 - L.ft) * fused_chain(F, False)) / F
+        W = CU["split4"] * P[H] + cu * (P[G] - P[H])
         J = H + (G - H + F - 1) // F
-        job = lambda i: B[i] * CHAIN["split4"] if i < H else B[H + (i - H) * F] * CHAIN[fk]
+
+        def job(i):
+            if i < H:
+                return B[i] * CHAIN["split4"]
+            g = H + (i - H) * F
+            return B[g] * fused_chain(F, L.job_together(g, F, G))
     m = max(W / C, job(0))
     if mode == 0 and 0 < H < G:
         m = max(m, job(H))
@@ -69,7 +106,7 @@ CHAIN32 = {k: np.float32(v) for k, v in CHAIN.items()}
 SIM_XCDS, SIM_CUS, SIM_MAX_G = 8, 32, 16384
 
 
-def sim_xcd(B, mode, H, F, x, per):
+def sim_xcd(B, mode, H, F, x, per, L=None):
     """plan_mixed_kernel's sim_xcd in the same fp32 operations: XCD x's jobs
     (x, x + 8, ..) started in order on whichever of its `per` CUs frees
     first; the time the last one frees."""
@@ -82,14 +119,16 @@ def sim_xcd(B, mode, H, F, x, per):
         elif j < H:
             p = np.float32(B[j]) * CHAIN32["split4"]
         else:
-            p = np.float32(B[H + (j - H) * F]) * CHAIN32[f"fused{F}"]
+            g = H + (j - H) * F
+            tg = L.job_together(g, F, G) if L is not None else True
+            p = np.float32(B[g]) * CHAIN32[f"fused{F}{'T' if tg else 'S'}"]
         nx = np.float32(t[0] + p)
         t = np.sort(np.append(t[1:], nx))
     return np.float32(t[-1]) if per else np.float32(0)
 
 
-def sim_plan(B, C, mode, H, F):
-    return max(sim_xcd(B, mode, H, F, x, C // SIM_XCDS) for x in range(SIM_XCDS))
+def sim_plan(B, C, mode, H, F, L=None):
+    return max(sim_xcd(B, mode, H, F, x, C // SIM_XCDS, L) for x in range(SIM_XCDS))
 
 
 def candidates(G, C, hcap, hb, fb):
@@ -117,12 +156,30 @@ def candidates(G, C, hcap, hb, fb):
     return out
 
 
-def model_plan(lengths, C, simulate=True):
+def together_bits(lengths, offsets, order):
+    """group_together of every sorted group: the span of its chunks'
+    addresses against their bytes."""
+    ln = np.asarray(lengths, np.int64)[order]
+    off = np.asarray(offsets, np.int64)[order]
+    n = ln.size
+    out = []
+    for g in range((n + 63) // 64):
+        o, L = off[64 * g:64 * g + 64], ln[64 * g:64 * g + 64]
+        out.append(int((o + L).max() - o.min()) <= 2 * int(L.sum()) + TOGETHER_SLACK)
+    return out
+
+
+def model_plan(lengths, C, simulate=True, offsets=None):
     """plan_mixed_kernel's search, restated: (estimate, mode, H, F).  The
-    lengths alone decide it (not where the chunks lie).  Stage 1 minimises
-    the makespan bounds; stage 2 simulates the dispatch of the candidate
-    plans and keeps the first shortest (estimate: its simulated time)."""
+    lengths and where each sorted group's chunks lie decide it (offsets:
+    the batch's; default: back to back in the given order, 64-byte steps).
+    Stage 1 minimises the makespan bounds; stage 2 simulates the dispatch of
+    the candidate plans and keeps the first shortest (estimate: its
+    simulated time).  Returns ((estimate, mode, H, F), (B, P, layout))."""
     lengths = np.asarray(lengths, np.int64)
+    if offsets is None:
+        offsets = np.zeros(lengths.size, np.int64)
+        offsets[1:] = np.cumsum((lengths + 63) // 64 * 64)[:-1]
     order = np.argsort(-lengths, kind="stable")  # the device's stable radix sort
     srt = lengths[order]
     B = [int(b) for b in total_blocks(srt[::64])]
@@ -130,29 +187,30 @@ def model_plan(lengths, C, simulate=True):
     P = [0]
     for b in B:
         P.append(P[-1] + b)
+    L = Layout(together_bits(lengths, offsets, order), B)
     hcap, grid = grid_of(G, C)
     best = None
     for H in list(range(hcap + 1)) + ([G] if G > hcap else []):
         for F in ((4, 8) if H < G else (4,)):
-            m = model_makespan(B, C, 0, H, F, P)
+            m = model_makespan(B, C, 0, H, F, P, L)
             if best is None or m < best[0]:
                 best = (m, 0, H, F)
     if not (simulate and G <= SIM_MAX_G and C % SIM_XCDS == 0 and C // SIM_XCDS <= SIM_CUS):
-        m = model_makespan(B, C, 1, 0, 0, P)
+        m = model_makespan(B, C, 1, 0, 0, P, L)
         if m < best[0]:
             best = (m, 1, 0, 0)
-        return best, (B, P)
+        return best, (B, P, L)
     cands = candidates(G, C, hcap, best[2], best[3])
-    s0 = sim_plan(B, C, *cands[0])
+    s0 = sim_plan(B, C, *cands[0], L)
     sims = [(s0,) + cands[0]]
     for m, h, f in cands[1:]:  # pass 2: only candidates whose bounds are below s0
-        lb = model_makespan(B, C, m, h, f, P)
-        sims.append((sim_plan(B, C, m, h, f) if lb < float(s0) else np.float32(np.inf), m, h, f))
+        lb = model_makespan(B, C, m, h, f, P, L)
+        sims.append((sim_plan(B, C, m, h, f, L) if lb < float(s0) else np.float32(np.inf), m, h, f))
     i = min(range(len(sims)), key=lambda k: (sims[k][0], k))
     if sims[2][0] <= np.float32(sims[i][0]) * np.float32(1.005):  # all-split near the best: taken
         i = 2
     mk, m, h, f = sims[i]
-    return (float(mk), m, 0 if m == 1 else h, 0 if m == 1 else f), (B, P)
+    return (float(mk), m, 0 if m == 1 else h, 0 if m == 1 else f), (B, P, L)
 
 
 def ragged(rng, n, long_n, long_lo, long_hi, short_hi, aligned=True):
@@ -286,9 +344,9 @@ def test_mixed_planner_matches_model(pkg, dev, cus, monkeypatch, capfd, shape):
                     torch.from_numpy(lens.astype(np.int32)).cuda(), dig)
     torch.cuda.synchronize()
     mode, H, F = _device_plan(capfd)
-    (best, bmode, bH, bF), (B, P) = model_plan(lens, cus)
+    (best, bmode, bH, bF), (B, P, L) = model_plan(lens, cus, offsets=off)
     simulated = len(B) <= SIM_MAX_G and cus % SIM_XCDS == 0 and cus // SIM_XCDS <= SIM_CUS
-    got = float(sim_plan(B, cus, mode, H, F)) if simulated else model_makespan(B, cus, mode, H, F, P)
+    got = float(sim_plan(B, cus, mode, H, F, L)) if simulated else model_makespan(B, cus, mode, H, F, P, L)
     assert got <= best * (1 + 1e-6), (shape, (mode, H, F), got, (bmode, bH, bF), best)
     # every chunk of these batches holds zeros: one digest per distinct length
     d = dig.cpu().numpy()
@@ -314,9 +372,9 @@ def test_mixed_beyond_simulated_group_count(pkg, dev, oracle, cus, monkeypatch, 
     got = run(pkg, torch, host, off, lens, {"SHA1CHUNK_MIXED_DEBUG": "1"}, monkeypatch)
     _check(got, want, "bounds-only plan")
     mode, H, F = _device_plan(capfd)
-    (best, bmode, bH, bF), (B, P) = model_plan(lens, cus)
+    (best, bmode, bH, bF), (B, P, L) = model_plan(lens, cus, offsets=off)
     assert len(B) > SIM_MAX_G
-    assert model_makespan(B, cus, mode, H, F, P) <= best * (1 + 1e-9), ((mode, H, F), (bmode, bH, bF))
+    assert model_makespan(B, cus, mode, H, F, P, L) <= best * (1 + 1e-9), ((mode, H, F), (bmode, bH, bF))
 
 
 def test_mixed_config5_law_at_4x(pkg, dev, oracle, cus, monkeypatch, dispatch):

@@ -61,7 +61,7 @@ def test_config5_law_plans(n, mode, lo, hi):
     "planner_sim"): 131072 the bounds' plan H = 257 17.36 ms, mode 1 14.36,
     H = 160 13.82; 262144 H = 115 19.99, H = 107 ~19.5."""
     lens = law(n)
-    (est, m, H, F), (B, _) = M.model_plan(lens, C)
+    (est, m, H, F), (B, _, _) = M.model_plan(lens, C)
     assert m == mode and (m == 1 or (lo <= H <= hi and F == 4)), (m, H, F)
     assert est >= B[0] * M.CHAIN["split4"]  # never below the longest chain
 
@@ -69,14 +69,15 @@ def test_config5_law_plans(n, mode, lo, hi):
 def test_simulation_rejects_late_long_fused_jobs():
     """At 131072 chunks the bounds alone pick H = 257 (> C: the 257th split
     group and the first long fused jobs start only when a CU frees); the
-    simulated dispatch puts that plan at 16.6 ms (measured 17.36) and picks
-    one near 13.1 (measured 14.36)."""
+    simulated dispatch puts that plan above 16 ms (measured 17.36 in round 2,
+    17.39 with H = 256 in round 4) and picks one near 14 (the 8-wave mode,
+    measured 14.16; round-4 constants, profiles/mixed_const_r04.jsonl)."""
     lens = law(131072)
-    (lb, m0, H0, F0), (B, P) = M.model_plan(lens, C, simulate=False)
+    (lb, m0, H0, F0), (B, P, L) = M.model_plan(lens, C, simulate=False)
     assert (m0, H0, F0) == (0, 257, 4)
-    assert M.sim_plan(B, C, 0, 257, 4) > 16000
+    assert M.sim_plan(B, C, 0, 257, 4, L) > 16000
     (est, m, H, F), _ = M.model_plan(lens, C)
-    assert est < 13500
+    assert est < 14500
 
 
 def test_sorted_insertion_sim_is_greedy_list_scheduling():
@@ -91,8 +92,9 @@ def test_sorted_insertion_sim_is_greedy_list_scheduling():
         if H == G:
             F = 4
         per = int(rng.choice([4, 32]))
-        J = [B[2 * j] * 0.80 for j in range((G + 1) // 2)] if mode == 1 else \
-            [B[j] * 0.742 for j in range(H)] + [B[j] * (1.28 if F == 4 else 2.43) for j in range(H, G, F)]
+        J = [B[2 * j] * M.CHAIN["split8"] for j in range((G + 1) // 2)] if mode == 1 else \
+            [B[j] * M.CHAIN["split4"] for j in range(H)] + \
+            [B[j] * M.CHAIN[f"fused{F}T"] for j in range(H, G, F)]
         for x in range(8):
             h = [0.0] * per
             for p in J[x::8]:
@@ -108,19 +110,35 @@ def test_model_rounds_bound_is_exact_for_equal_jobs():
     P = [0]
     for b in B:
         P.append(P[-1] + b)
-    m = M.model_makespan(B, C, 1, 0, 0, P)
+    m = M.model_makespan(B, C, 1, 0, 0, P, M.Layout([True] * G, B))
     assert m == pytest.approx(2 * 1025 * M.CHAIN["split8"])
 
 
-def test_plan_ignores_arrival_order():
-    """The plan is a function of the multiset of lengths: the device sorts
-    before planning, and the fused tail's shared loads make the layout
-    irrelevant to the choice (65536 x 512 KiB with permuted offsets: fused
-    tail 10.83 ms, in place 10.74; profiles/mixed_r02.json)."""
+def test_plan_depends_on_lengths_and_grouping_not_order():
+    """The device sorts before planning, so the caller's order of the
+    lengths does not matter when every sorted group's chunks lie scattered
+    (arrival layouts); what does is whether they lie together (round 4): a
+    batch laid out longest-first streams its fused tail lane-per-chunk."""
     lens = law(65536)
-    assert M.model_plan(lens, C)[0] == M.model_plan(np.sort(lens)[::-1].copy(), C)[0]
     rng = np.random.default_rng(3)
     assert M.model_plan(lens, C)[0] == M.model_plan(rng.permutation(lens), C)[0]
+    srt = np.sort(lens)[::-1].copy()
+    _, (_, _, L_arr) = M.model_plan(lens, C)
+    _, (_, _, L_srt) = M.model_plan(srt, C)
+    assert L_arr.ft < 0.1 and L_srt.ft > 0.9
+
+
+def test_longest_first_layout_takes_split_head_and_fused_tail():
+    """the config-5 law at 131072 chunks laid out
+    longest-first measured 13.10 ms with a 160-group split head + fused-4
+    tail against 13.63-13.82 for the 8-wave mode the layout-blind planner
+    picked (profiles/mixed_dispatch_ab_r03.json); arrival order keeps the
+    8-wave mode (13.80, the best measured there)."""
+    lens = law(131072)
+    (_, m_arr, _, _), _ = M.model_plan(lens, C)
+    (_, m_srt, H, F), _ = M.model_plan(np.sort(lens)[::-1].copy(), C)
+    assert m_arr == 1
+    assert m_srt == 0 and F == 4 and 64 <= H <= 256, (m_srt, H, F)
 
 
 @pytest.mark.parametrize("G", [257, 300, 511, 512, 513, 1024, 1025, 4096, 16384])
