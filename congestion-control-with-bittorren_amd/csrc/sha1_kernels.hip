@@ -405,17 +405,16 @@ __global__ __launch_bounds__(kLayoutThreads) void plan_layout_kernel(BatchArgs A
     }
 }
 
-// The planner's layout knowledge: one bit per group < kSimMaxG (in LDS), and
-// for the groups beyond, whether most blocks lie together.
+// The planner's layout knowledge: per group g < kSimMaxG (in LDS) how many
+// of groups g .. g+7 in a row lie together (groups past the batch count as
+// together, groups from kSimMaxG on as `rest`), and for the groups beyond,
+// whether most blocks lie together.
 struct PlanLayout {
-    const uint32_t* bits;
+    const uint8_t* run;
     bool rest;
-    __device__ bool together(uint32_t g) const { return g < kSimMaxG ? ((bits[g >> 5] >> (g & 31u)) & 1u) : rest; }
-    // a fused job of F groups from g streams lane-per-chunk if all of them do
+    // a fused job of F <= 8 groups from g streams lane-per-chunk if all of them do
     __device__ bool job_together(uint32_t g, uint32_t F, uint32_t G) const {
-        for (uint32_t i = g; i < min(g + F, G); ++i)
-            if (!together(i)) return false;
-        return true;
+        return g < kSimMaxG ? run[g] >= F : rest;
     }
 };
 
@@ -572,7 +571,17 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     }
     const uint64_t PG = scan[kPlanThreads - 1];
     const double ft = PG ? (double)tog_blocks / (double)PG : 1.0;
-    const PlanLayout L{togw, ft >= 0.5};
+    __shared__ uint8_t run8[kSimMaxG];
+    for (uint32_t g = t; g < min(G, kSimMaxG); g += kPlanThreads) {
+        uint32_t r = 0;
+        for (uint32_t i = g; i < g + 8u; ++i, ++r) {
+            const bool tg = i >= G || (i < kSimMaxG ? ((togw[i >> 5] >> (i & 31u)) & 1u) != 0 : ft >= 0.5);
+            if (!tg) break;
+        }
+        run8[g] = static_cast<uint8_t>(r);
+    }
+    __syncthreads();
+    const PlanLayout L{run8, ft >= 0.5};
     // P_H for every candidate H <= hcap, then each thread takes H = t, t + 1024, ..
     uint64_t P = scan[t] - local;  // P_{g0}
     for (uint32_t g = g0; g <= g1 && g <= hcap; ++g) {

@@ -1181,6 +1181,11 @@ struct s1be_vq {
     std::mutex mu;  // every entry point holds it: a queue may be shared by threads
     // batch mode's reservations: buffer -> (length, storage)
     std::unordered_map<void*, std::pair<uint32_t, std::unique_ptr<uint8_t[]>>> reserved;
+    // SHA1CHUNK_VQ_STATS=1: per entry point (submit, reserve, commit, release,
+    // poll, other) the calls, ns spent waiting for `mu` and ns holding it;
+    // printed as one JSON line to stderr by destroy (diagnostics)
+    bool stats = false;
+    uint64_t st_calls[6] = {}, st_wait_ns[6] = {}, st_hold_ns[6] = {};
 };
 
 namespace {
@@ -1345,6 +1350,8 @@ struct Pvq {
     std::unordered_map<uint64_t, uint64_t> held;  // reserved regions not released: ring offset -> id
     uint64_t slot_head = 0, slot_tail = 0, byte_head = 0, byte_tail = 0;
     uint32_t seen_done = 0;  // ctl->last_done at the last scan
+    // counters for SHA1CHUNK_VQ_STATS
+    uint64_t n_publish = 0, n_published = 0, n_copies = 0, n_launch = 0, n_scans = 0, n_sleeps = 0;
     int64_t alive_scan_ns = 0;  // pvq_ensure_drain: when it last read the alive words
     int alive_seen = 0;         // and how many it found (or launched)
     uint64_t open_slot0 = 0;
@@ -1409,6 +1416,7 @@ int pvq_launch(Pvq* P, int k, int wgs) {
     if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "vq drain launch: %s", hipGetErrorString(e));
     HIP_TRY(hipEventRecord(P->ended[k], P->stream[k]));
     P->launched[k] = true;
+    ++P->n_launch;
     return SHA1CHUNK_OK;
 }
 
@@ -1450,6 +1458,7 @@ int pvq_ensure_drain(Pvq* P) {
     if (P->alive_seen >= P->cus && now - P->alive_scan_ns < kAliveScanNs) return SHA1CHUNK_OK;
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
     const int alive = count_alive(P->ctl->alive[0], P->cus) + count_alive(P->ctl->alive[1], P->cus);
+    ++P->n_scans;
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
     P->alive_scan_ns = now;
     P->alive_seen = alive;
@@ -1488,8 +1497,10 @@ int pvq_stage(Pvq* P, uint64_t g, uint64_t slot0, uint32_t count) {
     HIP_TRY(hipSetDevice(P->dev));
     uint64_t run_at = 0, run_len = 0;
     auto flush = [&]() -> int {
-        if (run_len)
+        if (run_len) {
             HIP_TRY(hipMemcpyAsync(P->ddata + run_at, P->hdata + run_at, run_len, hipMemcpyHostToDevice, P->cstream));
+            ++P->n_copies;
+        }
         run_len = 0;
         return SHA1CHUNK_OK;
     };
@@ -1527,6 +1538,8 @@ int pvq_publish(Pvq* P) {
     ++P->inflight;
     const uint64_t slot0 = P->open_slot0;
     const uint32_t count = P->open_count;
+    ++P->n_publish;
+    P->n_published += count;
     P->open_slot0 = P->slot_tail;
     P->open_count = 0;
     if (P->dma) {
@@ -1622,6 +1635,7 @@ int pvq_wait(Pvq* P, Pred pred, const char* what, Stuck stuck) {
         if (P->inflight && (rc = pvq_ensure_drain(P))) return rc;
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
             return fail(SHA1CHUNK_EHIP, "vq: %s timed out (drain not progressing)", what);
+        ++P->n_sleeps;
         std::this_thread::sleep_for(std::chrono::microseconds(50));
     }
 }
@@ -2082,6 +2096,7 @@ void* s1be_vq_create(size_t batch, uint32_t max_chunk_len) {
     if (get_device(&D)) return nullptr;
     auto* q = new s1be_vq();
     q->dev = D->id;
+    q->stats = env_u64("SHA1CHUNK_VQ_STATS", 0) != 0;
     // the persistent drain unless SHA1CHUNK_VQ_MODE=batch (launch per batch)
     // or the device's drain CU budget is spent (then batch launches too)
     const char* mode = getenv("SHA1CHUNK_VQ_MODE");
@@ -2115,10 +2130,48 @@ void* s1be_vq_create(size_t batch, uint32_t max_chunk_len) {
     return q;
 }
 
+enum { kOpSubmit, kOpReserve, kOpCommit, kOpRelease, kOpPoll, kOpOther };
+struct VqLock {
+    s1be_vq* q;
+    int op;
+    int64_t t1 = 0;
+    VqLock(s1be_vq* q_, int op_) : q(q_), op(op_) {
+        if (!q->stats) {
+            q->mu.lock();
+            return;
+        }
+        const int64_t t0 = mono_ns();
+        q->mu.lock();
+        t1 = mono_ns();
+        ++q->st_calls[op];
+        q->st_wait_ns[op] += static_cast<uint64_t>(t1 - t0);
+    }
+    ~VqLock() {
+        if (q->stats) q->st_hold_ns[op] += static_cast<uint64_t>(mono_ns() - t1);
+        q->mu.unlock();
+    }
+};
+
+void vq_print_stats(const s1be_vq* q) {
+    static const char* names[6] = {"submit", "reserve", "commit", "release", "poll", "other"};
+    fprintf(stderr, "{\"vq_stats\": {");
+    for (int i = 0; i < 6; ++i)
+        fprintf(stderr, "\"%s\": [%llu, %.3f, %.3f], ", names[i], (unsigned long long)q->st_calls[i],
+                q->st_wait_ns[i] * 1e-6, q->st_hold_ns[i] * 1e-6);
+    const Pvq* P = q->pv;
+    if (P)
+        fprintf(stderr, "\"publish\": %llu, \"published\": %llu, \"copies\": %llu, \"launch\": %llu, "
+                "\"scans\": %llu, \"sleeps\": %llu, ",
+                (unsigned long long)P->n_publish, (unsigned long long)P->n_published,
+                (unsigned long long)P->n_copies, (unsigned long long)P->n_launch,
+                (unsigned long long)P->n_scans, (unsigned long long)P->n_sleeps);
+    fprintf(stderr, "\"units\": \"[calls, ms waiting for the lock, ms holding it]\"}}\n");
+}
+
 int s1be_vq_submit(void* qv, const void* chunk, uint32_t len, const uint8_t expected[20], uint64_t tag) {
     auto* q = static_cast<s1be_vq*>(qv);
     if (!q || (len && !chunk) || !expected) return fail(SHA1CHUNK_EINVAL, "vq: null argument");
-    std::lock_guard<std::mutex> lk(q->mu);
+    VqLock lk(q, kOpSubmit);
     if (q->pv) {
         if (len > q->pv->maxlen)
             return fail(SHA1CHUNK_EINVAL, "vq: chunk of %u bytes > max %u", len, q->pv->maxlen);
@@ -2133,7 +2186,7 @@ void* s1be_vq_reserve(void* qv, uint32_t len) {
         fail(SHA1CHUNK_EINVAL, "vq: null queue");
         return nullptr;
     }
-    std::lock_guard<std::mutex> lk(q->mu);
+    VqLock lk(q, kOpReserve);
     const uint32_t maxlen = q->pv ? q->pv->maxlen : q->maxlen;
     if (len > maxlen) {
         fail(SHA1CHUNK_EINVAL, "vq: reservation of %u bytes > max %u", len, maxlen);
@@ -2153,7 +2206,7 @@ void* s1be_vq_reserve(void* qv, uint32_t len) {
 int s1be_vq_commit(void* qv, void* buf, uint32_t len, const uint8_t expected[20], uint64_t tag) {
     auto* q = static_cast<s1be_vq*>(qv);
     if (!q || !buf || !expected) return fail(SHA1CHUNK_EINVAL, "vq: null argument");
-    std::lock_guard<std::mutex> lk(q->mu);
+    VqLock lk(q, kOpCommit);
     if (q->pv) return pvq_commit(q->pv, buf, len, expected, tag);
     auto it = q->reserved.find(buf);
     if (it == q->reserved.end()) return fail(SHA1CHUNK_EINVAL, "vq: %p is not a reserved buffer", buf);
@@ -2165,7 +2218,7 @@ int s1be_vq_commit(void* qv, void* buf, uint32_t len, const uint8_t expected[20]
 int s1be_vq_release(void* qv, void* buf) {
     auto* q = static_cast<s1be_vq*>(qv);
     if (!q || !buf) return fail(SHA1CHUNK_EINVAL, "vq: null argument");
-    std::lock_guard<std::mutex> lk(q->mu);
+    VqLock lk(q, kOpRelease);
     if (q->pv) return pvq_release(q->pv, buf);
     if (!q->reserved.erase(buf)) return fail(SHA1CHUNK_EINVAL, "vq: %p is not a reserved buffer", buf);
     return SHA1CHUNK_OK;
@@ -2174,27 +2227,28 @@ int s1be_vq_release(void* qv, void* buf) {
 int s1be_vq_flush(void* qv) {
     auto* q = static_cast<s1be_vq*>(qv);
     if (!q) return fail(SHA1CHUNK_EINVAL, "vq: null queue");
-    std::lock_guard<std::mutex> lk(q->mu);
+    VqLock lk(q, kOpOther);
     return q->pv ? pvq_publish(q->pv) : vq_batch_flush(q);
 }
 
 long s1be_vq_poll(void* qv, uint64_t* tags, uint8_t* mismatch, size_t max, int wait) {
     auto* q = static_cast<s1be_vq*>(qv);
     if (!q || (max && (!tags || !mismatch))) return fail(SHA1CHUNK_EINVAL, "vq: null argument");
-    std::lock_guard<std::mutex> lk(q->mu);
+    VqLock lk(q, kOpPoll);
     return q->pv ? pvq_poll(q->pv, tags, mismatch, max, wait) : vq_batch_poll(q, tags, mismatch, max, wait);
 }
 
 size_t s1be_vq_pending(const void* qv) {
     auto* q = static_cast<s1be_vq*>(const_cast<void*>(qv));
     if (!q) return 0;
-    std::lock_guard<std::mutex> lk(q->mu);
+    VqLock lk(q, kOpOther);
     return q->pv ? q->pv->pending : q->pending;
 }
 
 void s1be_vq_destroy(void* qv) {
     auto* q = static_cast<s1be_vq*>(qv);
     if (!q) return;
+    if (q->stats) vq_print_stats(q);
     if (q->pv) {
         pvq_destroy(q->pv);
         delete q;
