@@ -57,6 +57,13 @@
 #define PLAN_FUSED4S 1.408
 #define PLAN_FUSED8T 2.502
 #define PLAN_FUSED8S 2.661
+// The fused constants are measured with every CU running the fused shape
+// (tools/mixed_constants.sh).  In a mixed plan the fused workgroups share the
+// chip with split ones and run faster: fitted over the 26 forced split-head
+// plans of the config-5 law at 131072 and 262144 chunks in both layouts
+// (profiles/mixed_verify_r04c.jsonl), the fused jobs take 0.955 of their
+// all-fused time (simulated vs measured: rms 2.2 % instead of 4.5 %).
+#define PLAN_FUSED_SHARE 0.955
 
 // ---------------------------------------------------------------- lane ----
 __global__ __launch_bounds__(256) void sha1_lane_kernel(BatchArgs A) {
@@ -329,8 +336,8 @@ __global__ __launch_bounds__(kMixedThreads) void sha1_vq_drain_kernel(VqDrainArg
 // together and share each load across the wave when they lie scattered
 // (fused_coop_body), which costs a few per cent more: two constants each.
 constexpr double kChainSplit4 = PLAN_SPLIT4, kCuSplit4 = PLAN_SPLIT4;
-constexpr double kChainFused4T = PLAN_FUSED4T, kChainFused4S = PLAN_FUSED4S;
-constexpr double kChainFused8T = PLAN_FUSED8T, kChainFused8S = PLAN_FUSED8S;
+constexpr double kChainFused4T = PLAN_FUSED4T * PLAN_FUSED_SHARE, kChainFused4S = PLAN_FUSED4S * PLAN_FUSED_SHARE;
+constexpr double kChainFused8T = PLAN_FUSED8T * PLAN_FUSED_SHARE, kChainFused8S = PLAN_FUSED8S * PLAN_FUSED_SHARE;
 constexpr double kChainSplit8 = PLAN_SPLIT8, kCuSplit8 = PLAN_SPLIT8 / 2;
 
 __device__ __forceinline__ double fused_chain(uint32_t F, bool together) {
@@ -679,9 +686,49 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         if (x == 0 && (pass == 0 ? c == 0 : c >= 1)) cmk[c] = mk;
         __syncthreads();
     }
+    // Pass 3: heads next to the shortest split-head plan so far (same F;
+    // whichever plan is shortest overall).  The simulated
+    // time is jagged in H -- a head that fills the XCDs' CUs evenly beats its
+    // neighbours by several percent (config-5 law at 131072 chunks in
+    // arrival order: H = 187 simulated 13.88 ms and measured 13.92, mode 1
+    // 14.09 / 14.27, H = 176 14.35 / 14.41) and the grid above steps ~16
+    // heads, so every head within 8 of the best split-head plan is tried.
+    __shared__ uint32_t nref;
+    if (t == 0) {
+        uint32_t bi = kMaxCand;  // the shortest mode-0 candidate with a fused tail
+        for (uint32_t i = 0; i < ncand; ++i)
+            if (cmode[i] == 0 && chead[i] < G && (bi == kMaxCand || cmk[i] < cmk[bi])) bi = i;
+        uint32_t k = ncand;
+        if (bi < kMaxCand && cmk[bi] < __builtin_inff()) {
+            const uint32_t hb = chead[bi], fb = cf[bi];
+            for (uint32_t d = 1; d <= 8; ++d) {  // the grid steps ~16 heads
+                if (hb >= d && k < kMaxCand) {
+                    cmode[k] = 0;
+                    chead[k] = hb - d;
+                    cf[k++] = fb;
+                }
+                if (hb + d <= hcap && hb + d < G && k < kMaxCand) {
+                    cmode[k] = 0;
+                    chead[k] = hb + d;
+                    cf[k++] = fb;
+                }
+            }
+        }
+        nref = k;
+    }
+    __syncthreads();
+    {
+        const bool run = c >= ncand && c < nref;
+        float mk = __builtin_inff();
+        if (run) mk = sim_xcd(blocks, L, G, cmode[c], chead[c], cf[c], x, cus / kSimXcds);
+#pragma unroll
+        for (uint32_t m = 1; m < kSimXcds; m *= 2) mk = fmaxf(mk, __shfl_xor(mk, m));
+        if (x == 0 && run) cmk[c] = mk;
+        __syncthreads();
+    }
     if (t == 0) {
         uint32_t bi = 0;
-        for (uint32_t i = 1; i < ncand; ++i)
+        for (uint32_t i = 1; i < nref; ++i)
             if (cmk[i] < cmk[bi]) bi = i;
         // All-split (candidate 2) within 0.5 % of the best is taken instead:
         // a chain-bound batch then runs with no fused waves heating the chip

@@ -1350,6 +1350,8 @@ struct Pvq {
     std::unordered_map<uint64_t, uint64_t> held;  // reserved regions not released: ring offset -> id
     uint64_t slot_head = 0, slot_tail = 0, byte_head = 0, byte_tail = 0;
     uint32_t seen_done = 0;  // ctl->last_done at the last scan
+    std::mutex* mu = nullptr;  // the queue's lock (held by every caller; pvq_wait drops it to sleep)
+    std::mutex copy_mu;        // the copy helpers run one submit's copy at a time
     // counters for SHA1CHUNK_VQ_STATS
     uint64_t n_publish = 0, n_published = 0, n_copies = 0, n_launch = 0, n_scans = 0, n_sleeps = 0;
     int64_t alive_scan_ns = 0;  // pvq_ensure_drain: when it last read the alive words
@@ -1370,11 +1372,14 @@ struct Pvq {
     size_t hbytes = 0;
     unsigned hflags = 0;
     int budget_dev = -1;  // device whose drain CU budget this queue holds (pvq_create)
-    // DMA staging (SHA1CHUNK_VQ_DMA=1): the data ring lives in ordinary
-    // pinned host memory (`hdata`), each published group's chunks are copied
-    // by the copy engine into a device mirror of the ring (`ddata`, uncached
-    // device memory, the drain reads it from HBM), and the group is released
-    // to the drain (`pub`) once its copy event has completed.
+    // DMA staging (default since round 4; SHA1CHUNK_VQ_DMA=0 turns it off):
+    // the data ring lives in ordinary pinned host memory (`hdata`), each
+    // published group's chunks are copied by the copy engine into a device
+    // mirror of the ring (`ddata`, uncached device memory, the drain reads it
+    // from HBM), and the group is released to the drain (`pub`) once its copy
+    // event has completed.  The drain reading the ring over PCIe tops out at
+    // 26-28 GiB/s (8 receive threads, zero-copy), the copy engine at 37-45
+    // (profiles/vq_dma_r04.jsonl, vq_dma_knobs_r04.log).
     bool dma = false;
     uint8_t* hdata = nullptr;
     size_t hdata_bytes = 0;
@@ -1491,31 +1496,34 @@ int pvq_release_staged(Pvq* P) {
     return moved ? pvq_ensure_drain(P) : SHA1CHUNK_OK;
 }
 
-// Copy the chunks of slots [slot0, slot0 + count) into the device ring,
-// adjacent regions in one copy, and record the group's event.
+// Copy the chunks of slots [slot0, slot0 + count) into the device ring and
+// record the group's event.  Receive threads commit in their own order, so a
+// group's regions are sorted by ring offset and copied as runs, a run taking
+// in gaps of up to kStageGap bytes: one 512 KiB copy runs at ~30 GiB/s on the
+// copy engine (15-19 us, profiles), a run of many at the link's rate.  A
+// gap's bytes are other reservations' (filling, committed or free): their
+// device copy is rewritten with the same or later bytes before any group
+// that holds them is released to the drain, and none of them is in a group
+// the drain is hashing unless committed (whose bytes no longer change).
+constexpr uint64_t kStageGap = 1ull << 20;
+
 int pvq_stage(Pvq* P, uint64_t g, uint64_t slot0, uint32_t count) {
     HIP_TRY(hipSetDevice(P->dev));
-    uint64_t run_at = 0, run_len = 0;
-    auto flush = [&]() -> int {
-        if (run_len) {
-            HIP_TRY(hipMemcpyAsync(P->ddata + run_at, P->hdata + run_at, run_len, hipMemcpyHostToDevice, P->cstream));
-            ++P->n_copies;
-        }
-        run_len = 0;
-        return SHA1CHUNK_OK;
-    };
-    for (uint32_t j = 0; j < count; ++j) {
+    std::pair<uint64_t, uint64_t> rg[kPvqMaxGroup];  // (ring offset, end)
+    uint32_t n = 0;
+    for (uint32_t j = 0; j < count && n < kPvqMaxGroup; ++j) {
         const PvqRegion& r = P->regions[P->slot_reg[(slot0 + j) % P->nslots] - P->reg_base];
-        const uint64_t at = r.start % P->nbytes, len = r.end - r.start;
-        if (run_len && at == run_at + run_len) {
-            run_len += len;
-            continue;
-        }
-        if (int rc = flush()) return rc;
-        run_at = at;
-        run_len = len;
+        const uint64_t at = r.start % P->nbytes;
+        rg[n++] = {at, at + (r.end - r.start)};
     }
-    if (int rc = flush()) return rc;
+    std::sort(rg, rg + n);
+    for (uint32_t i = 0; i < n;) {
+        uint64_t run_at = rg[i].first, run_end = rg[i].second;
+        for (++i; i < n && rg[i].first <= run_end + kStageGap; ++i) run_end = std::max(run_end, rg[i].second);
+        HIP_TRY(hipMemcpyAsync(P->ddata + run_at, P->hdata + run_at, run_end - run_at, hipMemcpyHostToDevice,
+                               P->cstream));
+        ++P->n_copies;
+    }
     hipEvent_t ev;
     if (!P->spare_events.empty()) {
         ev = P->spare_events.back();
@@ -1636,7 +1644,12 @@ int pvq_wait(Pvq* P, Pred pred, const char* what, Stuck stuck) {
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
             return fail(SHA1CHUNK_EHIP, "vq: %s timed out (drain not progressing)", what);
         ++P->n_sleeps;
+        // sleep without the queue's lock: the other threads' commits, polls
+        // and releases are what frees the ring (each call re-checks its state
+        // after the wait)
+        if (P->mu) P->mu->unlock();
         std::this_thread::sleep_for(std::chrono::microseconds(50));
+        if (P->mu) P->mu->lock();
     }
 }
 template <typename Pred>
@@ -1826,7 +1839,7 @@ Pvq* pvq_create(Device* D, size_t batch, uint32_t max_chunk_len, int cus) {
     // with DMA staging the data ring is ordinary (cached) pinned memory of its
     // own, read only by the copy engine; the slot arrays and control words
     // stay in uncached memory the drain polls
-    P->dma = env_u64("SHA1CHUNK_VQ_DMA", 0) != 0;
+    P->dma = env_u64("SHA1CHUNK_VQ_DMA", 1) != 0;
     const size_t inline_data = P->dma ? 0 : P->nbytes;
     P->hbytes = inline_data + meta + sizeof(PvqCtl);
     P->hflags = ring_flags();
@@ -1942,12 +1955,25 @@ int pvq_enqueue(Pvq* P, uint64_t id, uint32_t len, const uint8_t expected[20], u
     return SHA1CHUNK_OK;
 }
 
+// The copy runs without the queue's lock (the region is this call's until
+// it is enqueued; nothing frees an uncollected region), on the helper
+// threads when no other submit is using them, else on the calling thread:
+// receive threads then copy side by side instead of one after another.
 int pvq_submit(Pvq* P, const void* chunk, uint32_t len, const uint8_t expected[20], uint64_t tag) {
     uint64_t id;
     if (int rc = pvq_alloc(P, len, false, &id)) return rc;
-    if (len)
-        pool_copy(*P->copier, P->data + P->regions[id - P->reg_base].start % P->nbytes,
-                  static_cast<const uint8_t*>(chunk), len);
+    if (len) {
+        uint8_t* dst = P->data + P->regions[id - P->reg_base].start % P->nbytes;
+        if (P->mu) P->mu->unlock();
+        {
+            std::unique_lock<std::mutex> cl(P->copy_mu, std::try_to_lock);
+            if (cl.owns_lock())
+                pool_copy(*P->copier, dst, static_cast<const uint8_t*>(chunk), len);
+            else
+                memcpy(dst, chunk, len);
+        }
+        if (P->mu) P->mu->lock();
+    }
     return pvq_enqueue(P, id, len, expected, tag);
 }
 
@@ -1995,7 +2021,11 @@ long pvq_poll(Pvq* P, uint64_t* tags, uint8_t* mismatch, size_t max, int wait) {
     int rc;
     if (wait) {
         if ((rc = pvq_publish(P))) return rc;
-        if ((rc = pvq_wait(P, [&] { return P->inflight == 0; }, "poll(wait)"))) return rc;
+        // every group published so far (other threads may keep publishing
+        // while this one sleeps; their later groups are not waited for)
+        const uint64_t target = P->next_g;
+        if ((rc = pvq_wait(P, [&] { return P->groups.empty() || P->groups.front().g >= target; }, "poll(wait)")))
+            return rc;
     } else {
         if ((rc = pvq_reap(P))) return rc;
         // an open group goes out once the device has room for it
@@ -2103,6 +2133,7 @@ void* s1be_vq_create(size_t batch, uint32_t max_chunk_len) {
     const int cus = mode && !strcmp(mode, "batch") ? 0 : drain_cus_take(D);
     if (cus > 0) {
         q->pv = pvq_create(D, batch, max_chunk_len, cus);
+        if (q->pv) q->pv->mu = &q->mu;
         if (!q->pv) {
             delete q;
             return nullptr;

@@ -25,8 +25,9 @@ def _plan_constants():
 
 
 _K = _plan_constants()
-CHAIN = {"split4": _K["split4"], "split8": _K["split8"], "fused4T": _K["fused4t"], "fused4S": _K["fused4s"],
-         "fused8T": _K["fused8t"], "fused8S": _K["fused8s"]}
+_SH = _K["fused_share"]  # the fused shapes' share-the-chip factor (PLAN_FUSED_SHARE)
+CHAIN = {"split4": _K["split4"], "split8": _K["split8"], "fused4T": _K["fused4t"] * _SH,
+         "fused4S": _K["fused4s"] * _SH, "fused8T": _K["fused8t"] * _SH, "fused8S": _K["fused8s"] * _SH}
 CU = {"split4": CHAIN["split4"], "split8": CHAIN["split8"] / 2}
 PLAN_MAX_H = 4096
 TOGETHER_SLACK = 2 << 20  # fused_coop_body: span <= 2 x bytes + 2 MiB
@@ -206,6 +207,16 @@ def model_plan(lengths, C, simulate=True, offsets=None):
     for m, h, f in cands[1:]:  # pass 2: only candidates whose bounds are below s0
         lb = model_makespan(B, C, m, h, f, P, L)
         sims.append((sim_plan(B, C, m, h, f, L) if lb < float(s0) else np.float32(np.inf), m, h, f))
+    # pass 3: heads next to the shortest split-head plan so far, same F
+    heads = [k for k in range(len(sims)) if sims[k][1] == 0 and sims[k][2] < G]
+    i = min(heads, key=lambda k: (sims[k][0], k)) if heads else None
+    if i is not None and np.isfinite(sims[i][0]):
+        hb, fb = sims[i][2], sims[i][3]
+        for d in range(1, 9):
+            if hb >= d and len(sims) < 128:
+                sims.append((sim_plan(B, C, 0, hb - d, fb, L), 0, hb - d, fb))
+            if hb + d <= hcap and hb + d < G and len(sims) < 128:
+                sims.append((sim_plan(B, C, 0, hb + d, fb, L), 0, hb + d, fb))
     i = min(range(len(sims)), key=lambda k: (sims[k][0], k))
     if sims[2][0] <= np.float32(sims[i][0]) * np.float32(1.005):  # all-split near the best: taken
         i = 2

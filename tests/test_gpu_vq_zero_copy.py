@@ -57,14 +57,17 @@ def _fill_in_place(view: np.ndarray, chunk: np.ndarray) -> None:
         view[o:o + PIECE] = chunk[o:o + PIECE]
 
 
-@pytest.mark.parametrize("mode", ["persistent", "batch"])
+@pytest.mark.parametrize("mode", ["persistent", "persistent-pcie", "batch"])
 def test_reserve_fill_commit_release(pkg, dev, corpus, monkeypatch, mode):
     """256 chunks through reserve -> in-place fill -> commit, up to 16
     sessions outstanding, every 5th chunk corrupted in its buffer before the
     commit; each result matches the golden digest's verdict, and each
     verified buffer still holds the chunk when its result comes back (the
-    job-buffer copy reads it) until it is released."""
-    monkeypatch.setenv("SHA1CHUNK_VQ_MODE", mode)
+    job-buffer copy reads it) until it is released.  persistent: the drain
+    reads groups the copy engine staged in HBM (default); persistent-pcie:
+    the drain reads the pinned ring over PCIe (SHA1CHUNK_VQ_DMA=0)."""
+    monkeypatch.setenv("SHA1CHUNK_VQ_MODE", mode.split("-")[0])
+    monkeypatch.setenv("SHA1CHUNK_VQ_DMA", "0" if mode.endswith("pcie") else "1")
     host, want = corpus
     n = 256
     held, results = {}, {}
@@ -236,6 +239,7 @@ def test_five_busy_queues_and_a_device_batch(pkg, dev, corpus, monkeypatch):
         buf = dev.empty(n * L512, dtype=dev.uint8, device="cuda")
         dig = dev.zeros((n, 20), dtype=dev.uint8, device="cuda")
         st = dev.cuda.Stream()
+        st.wait_stream(dev.cuda.current_stream())  # dig's zero fill runs on torch's stream
         pkg.synth_fill_device(buf, 0, n, L512, stream=st)
         t0 = time.perf_counter()
         pkg.hash_uniform_device(buf, L512, n, dig, stream=st)
