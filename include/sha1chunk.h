@@ -155,12 +155,17 @@ int sha1chunk_synth_fill_ragged_async(void *d_base, const uint64_t *d_offsets,
  * Default: a persistent drain kernel.  The chunks go into a ring in pinned
  * host memory (SHA1CHUNK_VQ_RING_MIB, default 1024) and are published in
  * groups of up to min(batch, 64); while fewer groups are in flight than the
- * drain has workgroups, each chunk goes out at once.  The drain, one
- * workgroup on each of SHA1CHUNK_VQ_CUS CUs (default 64), pulls the groups
- * over PCIe, hashes and compares them, and writes the results back to host
- * memory; it exits after SHA1CHUNK_VQ_IDLE_MS (default 20) without a claim
- * and the next submit starts it again.  A lone chunk comes back after its
- * own serial chain, with no batch to fill and no flush.
+ * drain has workgroups, each chunk goes out at once.  The copy engine
+ * stages each group into a mirror of the ring in device memory
+ * (SHA1CHUNK_VQ_DMA=0: the drain reads the pinned ring over PCIe instead).
+ * The drain, one workgroup on each of SHA1CHUNK_VQ_CUS CUs (default 64;
+ * all queues on a device share at most SHA1CHUNK_VQ_CU_BUDGET CUs, default
+ * half, and queues beyond it launch per batch), hashes and compares the
+ * groups and writes the results back to host memory; a workgroup exits
+ * after SHA1CHUNK_VQ_IDLE_MS (default 20) without a claim or after
+ * SHA1CHUNK_VQ_LIFE_MS (default 4) of work, and the next call starts it
+ * again.  A lone chunk comes back after its own serial chain, with no
+ * batch to fill and no flush.
  *
  * SHA1CHUNK_VQ_MODE=batch: batches are launched as kernels.  Once `batch`
  * submissions are pending (or on flush) the batch is hashed and

@@ -24,10 +24,14 @@ shutil.copy(f"{src}/trace/run_kernel_stats.csv", f"{dst}/rocprof_{name}_{out_tag
 shutil.copy(f"{src}/sq/run_counter_collection.csv", f"{dst}/rocprof_{name}_{out_tag}_sq_counters.csv")
 
 
+grid = sys.argv[4] if len(sys.argv) > 4 else None  # Grid_Size of the timed launches (other legs in the pass)
+
+
 def per_kernel(path, counter):
     vals = {}
     for r in csv.DictReader(open(path)):
-        if r["Counter_Name"] == counter and "sha1_" in r["Kernel_Name"] and "synth" not in r["Kernel_Name"]:
+        if r["Counter_Name"] == counter and "sha1_" in r["Kernel_Name"] and "synth" not in r["Kernel_Name"] \
+                and (grid is None or r["Grid_Size"] == grid):
             vals.setdefault(r["Kernel_Name"], []).append(float(r["Counter_Value"]))
     (k, v), = [(k, v) for k, v in vals.items()]
     return k, v
