@@ -797,9 +797,11 @@ def _cpu_baseline(O, n, L, golden, max_threads=None) -> dict:
     """The reference sha.c (oracle/_ref) on this host's cores over the same
     synthetic chunks as config 2 (chunks 0..4095, generated once): built -O2
     and with the reference Makefile's own flags (-g, no -O; Makefile:3), each
-    on 1 thread and on every usable core (chunk-strided pthreads); every row's
-    digests checked against the reference golden file.  `value` is the -O2
-    all-cores row.  Also the peer's per-chunk verify on one core."""
+    on 1 thread and on every usable core (chunk-strided pthreads), then the
+    repo's restatement (oracle/sha1_oracle.c) the same four ways; every row's
+    digests checked against the reference golden file.  `value` is the
+    reference -O2 all-cores row.  Also the peer's per-chunk verify on one
+    core."""
     cores = usable_cores()
     allc = cores["usable"] if max_threads is None else max(1, min(cores["usable"], max_threads))
     sample = min(n, 4096)
@@ -809,18 +811,24 @@ def _cpu_baseline(O, n, L, golden, max_threads=None) -> dict:
     want = np.fromfile(os.path.join(ROOT, "tests/golden/synth_4096x512k.bin"),
                        np.uint8).reshape(-1, 20)[:sample] if L == O.CHUNK_LEN else None
     rows = []
-    for opt in ("O2", "O0"):
-        for threads in (1, allc):
-            times, ok = [], True
-            # at least ~2 s of wall per row (one pass at 1 thread)
-            while len(times) < 5 and sum(times) < 2.0:
-                secs, dig = O.time_batch(data, off, ln, threads, opt)
-                times.append(secs)
-                ok &= want is not None and bool(np.array_equal(dig, want))
-            secs = float(np.median(times))
-            rows.append({"build": "-O2" if opt == "O2" else "reference Makefile flags (-g, -O0)",
-                         "threads": threads, "seconds": round(secs, 4), "passes": len(times),
-                         "GiBps": round(sample * L / secs / 2**30, 4), "parity": ok})
+    # the reference sha.c (kind "reference") on the whole sample; the repo's
+    # restatement (kind "port") on 1 thread over its first 1024
+    # chunks only, to keep the leg short
+    for kind in ("reference", "port"):
+        for opt in ("O2", "O0"):
+            for threads in (1, allc):
+                m = sample if kind == "reference" or threads > 1 else min(sample, 1024)
+                times, ok = [], True
+                # at least ~2 s of wall per row (one pass at 1 thread)
+                while len(times) < 5 and sum(times) < 2.0:
+                    secs, dig = O.time_batch(data[:m * L], off[:m], ln[:m], threads, opt, kind)
+                    times.append(secs)
+                    ok &= want is not None and bool(np.array_equal(dig, want[:m]))
+                secs = float(np.median(times))
+                rows.append({"kind": kind,
+                             "build": "-O2" if opt == "O2" else "reference Makefile flags (-g, -O0)",
+                             "threads": threads, "chunks": m, "seconds": round(secs, 4), "passes": len(times),
+                             "GiBps": round(m * L / secs / 2**30, 4), "parity": ok})
     one = [O.time_batch(data[i * L:(i + 1) * L], off[:1], ln[:1], 1, "O2")[0] for i in range(16)]
     head = rows[1]
     return {"value": head["GiBps"], "unit": "GiB/s", "cores": head["threads"], "kind": "reference",

@@ -41,9 +41,9 @@ def _declare(lib: C.CDLL, prefix: str) -> C.CDLL:
     getattr(lib, prefix + "time_synth").argtypes = [C.c_uint64, C.c_uint64, C.c_uint32,
                                                     C.c_uint64, C.c_int, _u8p]
     getattr(lib, prefix + "time_synth").restype = C.c_double
-    if prefix == "ref_":
-        lib.ref_time_batch.argtypes = [_u8p, _u64p, _u32p, C.c_size_t, _u8p, C.c_int]
-        lib.ref_time_batch.restype = C.c_double
+    tb = getattr(lib, prefix + "time_batch")
+    tb.argtypes = [_u8p, _u64p, _u32p, C.c_size_t, _u8p, C.c_int]
+    tb.restype = C.c_double
     return lib
 
 
@@ -65,6 +65,23 @@ def lib() -> C.CDLL:
         _lib.oracle_splitmix64.argtypes = [C.c_uint64]
         _lib.oracle_splitmix64.restype = C.c_uint64
     return _lib
+
+
+_port_o0 = None
+
+
+def port_lib(opt: str = "O2") -> C.CDLL | None:
+    """The restatement built -O2 (liboracle.so) or with the reference
+    Makefile's flags (liboracle_O0.so; None when not built)."""
+    global _port_o0
+    if opt == "O2":
+        return lib()
+    if _port_o0 is None:
+        path = os.path.join(HERE, "liboracle_O0.so")
+        if not os.path.exists(path):
+            return None
+        _port_o0 = _declare(C.CDLL(path), "oracle_")
+    return _port_o0
 
 
 def ref_lib(opt: str = "O2") -> C.CDLL | None:
@@ -130,18 +147,19 @@ def digest_of_digests(digests: np.ndarray) -> bytes:
 
 
 def time_batch(base: np.ndarray, offsets: np.ndarray, lengths: np.ndarray, threads: int = 1,
-               opt: str = "O2") -> tuple[float, np.ndarray]:
-    """Seconds for the reference sha.c (oracle/_ref, -O2 or its own Makefile
-    flags "O0") to hash a batch already in memory, and its digests."""
-    r = ref_lib(opt)
+               opt: str = "O2", kind: str = "reference") -> tuple[float, np.ndarray]:
+    """Seconds to hash a batch already in memory, and its digests: the
+    reference sha.c (kind "reference", oracle/_ref) or the restatement
+    (kind "port"), built -O2 or with the reference Makefile's flags ("O0")."""
+    r = ref_lib(opt) if kind == "reference" else port_lib(opt)
     if r is None:
-        raise FileNotFoundError(f"oracle/_ref reference build {opt} missing")
+        raise FileNotFoundError(f"{kind} build {opt} missing")
+    fn = r.ref_time_batch if kind == "reference" else r.oracle_time_batch
     base = np.ascontiguousarray(base, dtype=np.uint8)
     off = np.ascontiguousarray(offsets, dtype=np.uint64)
     ln = np.ascontiguousarray(lengths, dtype=np.uint32)
     out = np.zeros((len(off), 20), np.uint8)
-    secs = r.ref_time_batch(_p(base, _u8p), _p(off, _u64p), _p(ln, _u32p), len(off), _p(out, _u8p),
-                            threads)
+    secs = fn(_p(base, _u8p), _p(off, _u64p), _p(ln, _u32p), len(off), _p(out, _u8p), threads)
     return float(secs), out
 
 

@@ -204,3 +204,14 @@ double oracle_time_synth(uint64_t first, uint64_t count, uint32_t chunk_len, uin
     free(buf); free(off); free(len); free(dig);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* Seconds for oracle_hash_batch over a batch already in memory (the CPU
+ * baseline's restatement rows, bench.py). */
+double oracle_time_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, size_t n,
+                         uint8_t *dig, int threads) {
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    oracle_hash_batch(base, off, len, n, dig, threads);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

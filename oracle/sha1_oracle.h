@@ -44,6 +44,9 @@ void oracle_shahash(const uint8_t *p, int len, uint8_t out[20]);
  * Chunk-strided over `threads` pthreads (threads <= 1 -> calling thread). */
 void oracle_hash_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len,
                        size_t n, uint8_t *digests, int threads);
+/* oracle_hash_batch timed (seconds, CLOCK_MONOTONIC). */
+double oracle_time_batch(const uint8_t *base, const uint64_t *off, const uint32_t *len, size_t n,
+                         uint8_t *dig, int threads);
 
 /* Synthetic corpus: 64-bit little-endian word w of chunk c is
  * splitmix64(seed ^ (c << 24) ^ w); a trailing partial word keeps its low

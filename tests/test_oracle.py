@@ -177,3 +177,22 @@ def test_package_mixed_length_law(pkg, golden, oracle):
         assert hashlib.sha1(ln.tobytes()).hexdigest() == golden[key]["lengths_sha1"], key
         assert int(ln.astype(np.uint64).sum()) == golden[key]["total_bytes"]
     assert np.array_equal(pkg.sha1chunk.mixed_lengths(2000), oracle.mixed_lengths(2000))
+
+
+def test_cpu_baseline_builds_time_the_same_digests(oracle):
+    """bench.py's CPU baseline rows: the reference sha.c and
+    the restatement, each -O2 and with the reference Makefile's flags, time a
+    batch in memory on 1 and 2 threads and return the reference golden
+    digests of config 2's corpus."""
+    n, L = 4, oracle.CHUNK_LEN
+    data = oracle.synth_chunks(0, n, L)
+    off = np.arange(n, dtype=np.uint64) * L
+    ln = np.full(n, L, np.uint32)
+    want = np.fromfile(os.path.join(os.path.dirname(__file__), "golden", "synth_4096x512k.bin"),
+                       np.uint8).reshape(-1, 20)[:n]
+    kinds = ["port"] + (["reference"] if oracle.ref_lib("O2") is not None else [])
+    for kind in kinds:
+        for opt in ("O2", "O0"):
+            for threads in (1, 2):
+                secs, dig = oracle.time_batch(data, off, ln, threads, opt, kind)
+                assert secs > 0 and np.array_equal(dig, want), (kind, opt, threads)
