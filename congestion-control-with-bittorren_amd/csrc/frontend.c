@@ -117,6 +117,8 @@ static void be_load(void) {
     BE.name = (ret(*) args)dlsym(h, "s1be_" #name);                                               \
     if (!BE.name) {                                                                               \
         snprintf(be_err, sizeof be_err, "HIP backend %.400s lacks s1be_" #name, path);                \
+        memset(&BE, 0, sizeof BE);                                                                \
+        dlclose(h);                                                                               \
         return;                                                                                   \
     }
     BACKEND_FUNCS(BE_SYM)
