@@ -430,9 +430,11 @@ __device__ __forceinline__ void read_w_group(const uint8_t* slot, uint32_t (&W)[
 // memory instead of LDS, wave 1 left empty instead of wave 2, the 8-wave
 // layout split over the LDS store-path halves, and variants in which the
 // consumer skipped its LDS reads or one side idled at the barriers (wrong
-// digests by design).  profiles/issue_r01.json, split_variants_r01.json,
+// digests by design); round 4: one schedule read every 4 rounds instead of
+// bursts (6.49 against 6.03 ms at 4096 chunks in the one-group shape, 6.60
+// against 6.31 at 32768 in the 8-wave one: spread_read_ab_r04.json).  profiles/issue_r01.json, split_variants_r01.json,
 // split_2prod_sweep_r01.json, split_prio_read_r02.json, global_w_ab_r02.json,
-// halves_ab_r03.json.  Shapes other than the product's 1 / 4 / 11 are built
+// halves_ab_r03.json, spread_read_ab_r04.json.  Shapes other than the product's 1 / 4 / 11 are built
 // only into the A/B library (tools/ab_kernels.hip, `make ab`).
 constexpr int kVWK = 1;      // producer ships W+K (consumer: one VOP2 add)
 constexpr int kVUnmask = 4;  // unmasked commit while every lane is live
