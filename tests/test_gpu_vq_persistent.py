@@ -29,9 +29,13 @@ def dev(pkg):
     return torch
 
 
-@pytest.fixture
-def persistent(monkeypatch):
+@pytest.fixture(params=["staged", "pcie"])
+def persistent(request, monkeypatch):
+    """The persistent drain on both data paths: groups staged in HBM by the
+    copy engine (default) or read from the pinned ring over PCIe
+    (SHA1CHUNK_VQ_DMA=0)."""
     monkeypatch.setenv("SHA1CHUNK_VQ_MODE", "persistent")
+    monkeypatch.setenv("SHA1CHUNK_VQ_DMA", "1" if request.param == "staged" else "0")
 
 
 def _poll_until(q, n, timeout=30.0):
