@@ -183,13 +183,18 @@ int sha1chunk_synth_fill_ragged_async(void *d_base, const uint64_t *d_offsets,
  * required.
  *
  * Every queue call takes the queue's lock, so several threads (receive
- * sessions) may share one queue.  Persistent drains of all queues on one
- * device hold at most SHA1CHUNK_VQ_CU_BUDGET CUs (default half the device);
- * a queue created when that budget is spent uses batch launches.  The copy
- * of submit() is split over SHA1CHUNK_VQ_THREADS threads (default 4, the
- * caller included: three helper threads per queue that spin briefly between
- * submissions); reserve/commit has no copy.  Measured on 16384 x 512 KiB host chunks: 26-35 GiB/s
- * persistent, 23-37 GiB/s batch. */
+ * sessions) may share one queue; a call that waits (for ring space, or
+ * poll(wait)) and submit()'s copy release the lock meanwhile, so the other
+ * threads' calls go on.  destroy() must not overlap any other call on the
+ * queue.  Persistent drains of all queues on one device hold at most
+ * SHA1CHUNK_VQ_CU_BUDGET CUs (default half the device); a queue created
+ * when that budget is spent uses batch launches.  The copy of submit() runs
+ * on SHA1CHUNK_VQ_THREADS threads (default 4, the caller included: three
+ * helper threads per queue that spin briefly between submissions) when no
+ * other submit is using them, else on the calling thread; reserve/commit
+ * has no copy.  Measured on 16384 x 512 KiB host chunks from 4-8 receive
+ * threads: 45-48 GiB/s reserve/commit, 22-25 GiB/s submit (DESIGN.md
+ * section 9). */
 typedef struct sha1chunk_vq sha1chunk_vq;
 /* NULL on failure (sha1chunk_last_error() says why). */
 sha1chunk_vq *sha1chunk_vq_create(size_t batch, uint32_t max_chunk_len);
@@ -213,8 +218,9 @@ int sha1chunk_vq_commit(sha1chunk_vq *q, void *buf, uint32_t len, const uint8_t 
                         uint64_t tag);
 int sha1chunk_vq_release(sha1chunk_vq *q, void *buf);
 int sha1chunk_vq_flush(sha1chunk_vq *q);
-/* Up to max finished results; wait != 0 blocks until everything submitted so
- * far has finished.  Returns the number written (>= 0) or a negative error. */
+/* Up to max finished results; wait != 0 blocks until everything submitted
+ * before the call has finished (later submissions from other threads are not
+ * waited for).  Returns the number written (>= 0) or a negative error. */
 long sha1chunk_vq_poll(sha1chunk_vq *q, uint64_t *tags, uint8_t *mismatch, size_t max, int wait);
 /* Submitted but not yet returned by poll(). */
 size_t sha1chunk_vq_pending(const sha1chunk_vq *q);
