@@ -559,60 +559,88 @@ def _chain_floor_ms(length: int) -> float:
     return blocks * CONSUMER_INSTR_PER_BLOCK * ISSUE_CYCLES / CLOCK_HZ * 1e3
 
 
-def _mixed_run(pkg, torch, lens: np.ndarray, reps: int = 5, warm: int = 2) -> dict:
+def _mixed_run(pkg, torch, lens: np.ndarray, reps: int = 5, warm: int = 2, layout: str = "arrival",
+               forced=()) -> dict:
     """A device-resident mixed-length batch (chunk i = synthetic chunk i at
-    lens[i] bytes, 128-byte aligned back to back) through AUTO -- the
-    length sort and, above one group of 64 per CU, the mixed kernel's
-    persistent dispatch with its device-side plan.  Timed with HIP events on
-    the call's stream (sort + hash), median of `reps` after `warm`."""
+    lens[i] bytes, 128-byte aligned) through AUTO -- the length sort and,
+    above one group of 64 per CU, the mixed kernel's persistent dispatch
+    with its device-side plan.  layout "arrival": the chunks back to back in
+    index order (as received); "longest_first": back to back in descending
+    length order (the same chunks and digests, laid out so every sorted
+    group's chunks lie together).  `forced`: plans ("mode,H,F") run through
+    SHA1CHUNK_MIXED_PLAN on the same buffer after AUTO, for comparison.
+    Timed with HIP events on the call's stream (sort + plan + hash), median
+    of `reps` after `warm`."""
     n = int(lens.size)
-    off, total = pkg.sha1chunk.ragged_layout(lens)
+    if layout == "arrival":
+        off, total = pkg.sha1chunk.ragged_layout(lens)
+    else:
+        order = np.argsort(-lens.astype(np.int64), kind="stable")
+        o2, total = pkg.sha1chunk.ragged_layout(lens[order])
+        off = np.empty_like(o2)
+        off[order] = o2
     st = torch.cuda.Stream()
     d_base = torch.zeros(total + 128, dtype=torch.uint8, device="cuda")
     d_off = torch.from_numpy(off.astype(np.int64)).cuda()
     d_len = torch.from_numpy(lens.astype(np.int32)).cuda()
     dig = torch.zeros((n, 20), dtype=torch.uint8, device="cuda")
+    st.wait_stream(torch.cuda.current_stream())  # the zero fills and copies above run on torch's stream
     pkg.synth_fill_ragged_device(d_base, d_off, d_len, 0, stream=st)
     torch.cuda.synchronize()
-    for _ in range(warm):
-        pkg.hash_device(d_base, d_off, d_len, dig, stream=st)
-    torch.cuda.synchronize()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(reps)]
-    t0 = time.perf_counter()
-    for e0, e1 in evs:
-        e0.record(st)
-        pkg.hash_device(d_base, d_off, d_len, dig, stream=st)
-        e1.record(st)
-    torch.cuda.synchronize()
-    wall = (time.perf_counter() - t0) / reps
-    ms = float(np.median([e0.elapsed_time(e1) for e0, e1 in evs]))
-    # the plan the runtime chose (one more, untimed call with the debug line on)
-    plan = None
-    os.environ["SHA1CHUNK_MIXED_DEBUG"] = "1"
-    try:
-        with _CaptureStderr() as cap:
+
+    def timed():
+        for _ in range(warm):
             pkg.hash_device(d_base, d_off, d_len, dig, stream=st)
-            torch.cuda.synchronize()
-    finally:
-        del os.environ["SHA1CHUNK_MIXED_DEBUG"]
-    for line in cap.text.splitlines():
-        if line.startswith("sha1chunk mixed plan:"):
-            plan = line.split(":", 1)[1].strip()
-    got = dig.cpu().numpy()
+        torch.cuda.synchronize()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(reps)]
+        t0 = time.perf_counter()
+        for e0, e1 in evs:
+            e0.record(st)
+            pkg.hash_device(d_base, d_off, d_len, dig, stream=st)
+            e1.record(st)
+        torch.cuda.synchronize()
+        wall = (time.perf_counter() - t0) / reps
+        # the plan the runtime used (one more, untimed call with the debug line on)
+        plan = None
+        os.environ["SHA1CHUNK_MIXED_DEBUG"] = "1"
+        try:
+            with _CaptureStderr() as cap:
+                pkg.hash_device(d_base, d_off, d_len, dig, stream=st)
+                torch.cuda.synchronize()
+        finally:
+            del os.environ["SHA1CHUNK_MIXED_DEBUG"]
+        for line in cap.text.splitlines():
+            if line.startswith("sha1chunk mixed plan:"):
+                plan = line.split(":", 1)[1].strip()
+        return float(np.median([e0.elapsed_time(e1) for e0, e1 in evs])), wall, plan, dig.cpu().numpy()
+
+    ms, wall, plan, got = timed()
+    vs = {}
+    for f in forced:
+        os.environ["SHA1CHUNK_MIXED_PLAN"] = f
+        try:
+            fms, _, fplan, fgot = timed()
+        finally:
+            del os.environ["SHA1CHUNK_MIXED_PLAN"]
+        vs[f] = {"kernel_ms": round(fms, 4), "plan": fplan, "auto_over_forced": round(ms / fms, 4),
+                 "same_digests": bool(np.array_equal(fgot, got))}
     payload = int(lens.astype(np.uint64).sum())
     longest = int(lens.max())
     floor = _chain_floor_ms(longest)
     del d_base, d_off, d_len, dig
     torch.cuda.empty_cache()
-    return {"chunks": n, "payload_bytes": payload, "kernel_ms": round(ms, 4),
-            "wall_ms_per_call": round(wall * 1e3, 4),
-            "payload_GiBps": round(payload / (ms * 1e-3) / 2**30, 2),
-            "hbm_frac": round((payload + 20 * n) / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 5),
-            "longest_chunk_bytes": longest, "longest_chain_floor_ms": round(floor, 4),
-            "floor_frac": round(floor / ms, 4),
-            "plan": plan or "no mixed kernel (<= one group of 64 per CU: split shape)",
-            "_digests": got}
+    out = {"chunks": n, "layout": layout, "payload_bytes": payload, "kernel_ms": round(ms, 4),
+           "wall_ms_per_call": round(wall * 1e3, 4),
+           "payload_GiBps": round(payload / (ms * 1e-3) / 2**30, 2),
+           "hbm_frac": round((payload + 20 * n) / (ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 5),
+           "longest_chunk_bytes": longest, "longest_chain_floor_ms": round(floor, 4),
+           "floor_frac": round(floor / ms, 4),
+           "plan": plan or "no mixed kernel (<= one group of 64 per CU: split shape)",
+           "_digests": got}
+    if vs:
+        out["forced"] = vs
+    return out
 
 
 def _config5_leg(pkg, torch, golden) -> dict:
@@ -620,7 +648,9 @@ def _config5_leg(pkg, torch, golden) -> dict:
     shape, packet_handler.c:469-472 -> job.c:217-228): the 16384-chunk batch
     checked digest by digest against the reference's golden file, and the
     same length law at 4x (65536 chunks, the persistent mixed kernel's
-    regime) against its reference golden aggregate."""
+    regime) against its reference golden aggregate, and at 8x (131072) in
+    arrival and longest-first layouts, each beside a forced plan (the mixed
+    planner's layout- and clock-aware choice, VERDICT r3 next #8)."""
     import hashlib
     lens = np.fromfile(os.path.join(ROOT, "tests/golden/mixed_16384_len.bin"), "<u4")
     want = np.fromfile(os.path.join(ROOT, "tests/golden/mixed_16384.bin"), np.uint8).reshape(-1, 20)
@@ -639,6 +669,19 @@ def _config5_leg(pkg, torch, golden) -> dict:
                              hashlib.sha1(d.tobytes()).hexdigest() == g4["agg"])
         r64["parity_ref"] = "digest-of-digests == golden config5x4.agg (reference sha.c)"
         out["n65536"] = r64
+    g8 = golden.get("config5x8")
+    if g8:
+        # the law at 8x in both layouts, AUTO against the best forced plan of
+        # the round-4 grids (tools/mixed_verify.sh: H = 187, F = 4 in both)
+        lens8 = pkg.sha1chunk.mixed_lengths(g8["chunks"])
+        ok_l8 = hashlib.sha1(lens8.tobytes()).hexdigest() == g8["lengths_sha1"]
+        for lay in ("arrival", "longest_first"):
+            r = _mixed_run(pkg, torch, lens8, layout=lay, forced=("0,187,4",))
+            d = r.pop("_digests")
+            r["parity"] = bool(ok_l8 and hashlib.sha1(d.tobytes()).hexdigest() == g8["agg"] and
+                               all(v["same_digests"] for v in r["forced"].values()))
+            r["parity_ref"] = "digest-of-digests == golden config5x8.agg (reference sha.c); forced plans: same digests"
+            out[f"n131072_{lay}"] = r
     out["parity"] = all(v["parity"] for k, v in out.items() if k.startswith("n"))
     return out
 

@@ -17,7 +17,7 @@ Outputs (small; committed):
   mixed_16384.bin         all digests of BASELINE config 5 (mixed lengths)
   mixed_16384_len.bin     its 16384 chunk lengths (uint32 LE)
 
-`python tests/golden/make_golden.py --add config5x4` adds only the 4x config-5
+`python tests/golden/make_golden.py --add config5x4` (or config5x8) adds only the 4x (8x) config-5
 aggregate (65536 chunks of the same length law, bench.py's config5 leg) to an
 existing golden.json.
 """
@@ -105,27 +105,31 @@ def mixed_golden(n: int) -> dict:
             "sample": {str(i): dig[i].tobytes().hex() for i in sample}}
 
 
-def add_config5x4() -> None:
+def add_config5x(k: int) -> None:
+    """golden["config5x<k>"]: the config-5 law at k x 16384 chunks."""
     O.build(ref=True)
     assert O.ref_lib() is not None, "reference build failed"
     path = os.path.join(OUT, "golden.json")
     g = json.load(open(path))
     t0 = time.time()
-    g["config5x4"] = mixed_golden(4 * 16384)
-    # its first 16384 chunks are config 5 itself
+    name = f"config5x{k}"
+    g[name] = mixed_golden(k * 16384)
+    # its first 16384 chunks are config 5 itself, its first 65536 config5x4
     d5 = np.fromfile(os.path.join(OUT, "mixed_16384.bin"), np.uint8).reshape(-1, 20)
-    for k, v in g["config5x4"]["sample"].items():
-        if int(k) < 16384:
-            assert d5[int(k)].tobytes().hex() == v, k
-    print(f"config5x4 {time.time() - t0:.1f}s", flush=True)
+    for i, v in g[name]["sample"].items():
+        if int(i) < 16384:
+            assert d5[int(i)].tobytes().hex() == v, i
+        if k != 4 and "config5x4" in g and i in g["config5x4"]["sample"]:
+            assert g["config5x4"]["sample"][i] == v, i
+    print(f"{name} {time.time() - t0:.1f}s", flush=True)
     with open(path, "w") as f:
         json.dump(g, f, indent=1, sort_keys=True)
     print("wrote", path)
 
 
 def main() -> None:
-    if sys.argv[1:] == ["--add", "config5x4"]:
-        return add_config5x4()
+    if len(sys.argv) == 3 and sys.argv[1] == "--add" and sys.argv[2].startswith("config5x"):
+        return add_config5x(int(sys.argv[2][len("config5x"):]))
     O.build(ref=True)
     assert O.ref_lib() is not None, "reference build failed"
     g: dict = {"seed": O.SEED, "chunk_len": O.CHUNK_LEN,
