@@ -536,6 +536,10 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     const uint32_t n = A.n;
     const uint32_t t = threadIdx.x;
     if (t == 0) plan[3] = 0u;  // the persistent kernel's job counter
+    // stage end times (s_memrealtime, 100 MHz; plan[8..13], thread 0) for
+    // SHA1CHUNK_MIXED_DEBUG: scan, bounds search, passes 1, 2, 3
+    uint64_t ts[6] = {0, 0, 0, 0, 0, 0};
+    if (t == 0) ts[0] = __builtin_amdgcn_s_memrealtime();
     if (forced) {
         if (t == 0) {
             plan[0] = fmode;
@@ -578,6 +582,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     }
     const uint64_t PG = scan[kPlanThreads - 1];
     const double ft = PG ? (double)tog_blocks / (double)PG : 1.0;
+    if (t == 0) ts[1] = __builtin_amdgcn_s_memrealtime();
     __shared__ uint8_t run8[kSimMaxG];
     for (uint32_t g = t; g < min(G, kSimMaxG); g += kPlanThreads) {
         uint32_t r = 0;
@@ -624,6 +629,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         }
         __syncthreads();
     }
+    if (t == 0) ts[2] = __builtin_amdgcn_s_memrealtime();
     const bool simulate = G <= kSimMaxG && cus % kSimXcds == 0 && cus / kSimXcds <= kSimCus;
     if (!simulate) {
         if (t == 0) {
@@ -631,6 +637,8 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
             plan[0] = split8 ? 1u : 0u;
             plan[1] = split8 ? 0u : best_h[0];
             plan[2] = split8 ? 0u : best_f[0];
+#pragma unroll
+            for (int i = 8; i < 13; ++i) plan[i] = 0u;  // no simulation stages
         }
         return;
     }
@@ -685,6 +693,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         for (uint32_t m = 1; m < kSimXcds; m *= 2) mk = fmaxf(mk, __shfl_xor(mk, m));
         if (x == 0 && (pass == 0 ? c == 0 : c >= 1)) cmk[c] = mk;
         __syncthreads();
+        if (t == 0) ts[3 + pass] = __builtin_amdgcn_s_memrealtime();
     }
     // Pass 3: heads next to the shortest split-head plan so far (same F;
     // whichever plan is shortest overall).  The simulated
@@ -725,6 +734,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         for (uint32_t m = 1; m < kSimXcds; m *= 2) mk = fmaxf(mk, __shfl_xor(mk, m));
         if (x == 0 && run) cmk[c] = mk;
         __syncthreads();
+        if (t == 0) ts[5] = __builtin_amdgcn_s_memrealtime();
     }
     if (t == 0) {
         uint32_t bi = 0;
@@ -738,6 +748,8 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         plan[0] = cmode[bi];
         plan[1] = cmode[bi] == 1 ? 0u : chead[bi];
         plan[2] = cmode[bi] == 1 ? 0u : cf[bi];
+#pragma unroll
+        for (int i = 1; i < 6; ++i) plan[7 + i] = static_cast<uint32_t>(ts[i] - ts[0]);
     }
 }
 
