@@ -602,7 +602,7 @@ def _mixed_run(pkg, torch, lens: np.ndarray, reps: int = 5, warm: int = 2, layou
         torch.cuda.synchronize()
         wall = (time.perf_counter() - t0) / reps
         # the plan the runtime used (one more, untimed call with the debug line on)
-        plan = None
+        plan = stages = None
         os.environ["SHA1CHUNK_MIXED_DEBUG"] = "1"
         try:
             with _CaptureStderr() as cap:
@@ -613,14 +613,17 @@ def _mixed_run(pkg, torch, lens: np.ndarray, reps: int = 5, warm: int = 2, layou
         for line in cap.text.splitlines():
             if line.startswith("sha1chunk mixed plan:"):
                 plan = line.split(":", 1)[1].strip()
-        return float(np.median([e0.elapsed_time(e1) for e0, e1 in evs])), wall, plan, dig.cpu().numpy()
+            if line.startswith("sha1chunk mixed planner stages:"):
+                stages = line.split(":", 1)[1].strip()
+        return (float(np.median([e0.elapsed_time(e1) for e0, e1 in evs])), wall, plan, dig.cpu().numpy(),
+                stages)
 
-    ms, wall, plan, got = timed()
+    ms, wall, plan, got, stages = timed()
     vs = {}
     for f in forced:
         os.environ["SHA1CHUNK_MIXED_PLAN"] = f
         try:
-            fms, _, fplan, fgot = timed()
+            fms, _, fplan, fgot, _ = timed()
         finally:
             del os.environ["SHA1CHUNK_MIXED_PLAN"]
         vs[f] = {"kernel_ms": round(fms, 4), "plan": fplan, "auto_over_forced": round(ms / fms, 4),
@@ -638,6 +641,8 @@ def _mixed_run(pkg, torch, lens: np.ndarray, reps: int = 5, warm: int = 2, layou
            "floor_frac": round(floor / ms, 4),
            "plan": plan or "no mixed kernel (<= one group of 64 per CU: split shape)",
            "_digests": got}
+    if stages:  # the planner's stage end times in the untimed debug call (us since its start)
+        out["planner_stages_untimed_call"] = stages
     if vs:
         out["forced"] = vs
     return out
