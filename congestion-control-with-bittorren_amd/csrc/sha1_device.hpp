@@ -45,6 +45,19 @@ __device__ __forceinline__ uint32_t chf(uint32_t b, uint32_t c, uint32_t d) {
     return d ^ (b & (c ^ d));
 }
 __device__ __forceinline__ uint32_t bswap(uint32_t x) { return __builtin_bswap32(x); }
+// The same byte swap (one v_perm_b32), its result forced into a register
+// other than its source's.  For a prefetched stage that is swapped into the
+// schedule window and then refilled by the next load: with bswap() hipcc
+// swaps the stage's second half in place and keeps those registers as the
+// window through the compression, so the refill lands elsewhere and is
+// copied back once per trip (8 v_mov_b64 per block in the fused loop); here
+// the stage registers die at the swap and the refill targets them directly
+// (621.75 -> 613.75 VALU per block, profiles/fused_vmov_r04.json).
+__device__ __forceinline__ uint32_t bswap_fresh(uint32_t x) {
+    uint32_t r;
+    asm("v_perm_b32 %0, %1, %1, %2" : "=&v"(r) : "v"(x), "s"(0x00010203u));
+    return r;
+}
 
 // Round t (compile-time after unrolling) over the five-word state v[], kept
 // in place: a = v[(0-t)%5] ... e = v[(4-t)%5]; the new a lands in e's slot

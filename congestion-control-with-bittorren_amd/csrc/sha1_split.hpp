@@ -746,7 +746,7 @@ __device__ __forceinline__ void fused_stage(uint32_t s, uint32_t S, const Entry&
     for (int half = 0; half < 2; ++half) {
         uint32_t w[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) w[j] = bswap(cur.w[16 * half + j]);
+        for (int j = 0; j < 16; ++j) w[j] = bswap_fresh(cur.w[16 * half + j]);
         if (half == 1 && s + 2 < S) load_stage<V>(en.p + 128ull * (s + 2), cur);
         compress(h, w);
     }
@@ -776,11 +776,11 @@ __device__ __forceinline__ void fused_stage_any(uint32_t s, uint32_t S, const En
     uint32_t w[16];
     shift_raw<32, 0, 16>(cur, sh, w);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
+    for (int j = 0; j < 16; ++j) w[j] = bswap_fresh(w[j]);
     compress(h, w);
     shift_raw<32, 16, 16>(cur, sh, w);
 #pragma unroll
-    for (int j = 0; j < 16; ++j) w[j] = bswap(w[j]);
+    for (int j = 0; j < 16; ++j) w[j] = bswap_fresh(w[j]);
     if (s + 2 < S) load_raw<32>(en.p + 128ull * (s + 2), cur);
     compress(h, w);
 }
@@ -831,7 +831,7 @@ __device__ __forceinline__ void coop_compress(const uint32_t (&cur)[32], uint32_
     for (int half = 0; half < 2; ++half) {
         uint32_t w[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) w[j] = bswap(cur[16 * half + j]);
+        for (int j = 0; j < 16; ++j) w[j] = bswap_fresh(cur[16 * half + j]);
         compress(h, w);
     }
 }
