@@ -55,16 +55,16 @@ __device__ __forceinline__ void emit(const BatchArgs& A, uint32_t id, const uint
 // prefetched), then the padded tail (unless the batch is in update mode).
 __device__ __forceinline__ void lane_loop(const Entry& en, uint32_t k0, uint32_t (&h)[5]) {
     const uint32_t nfull = en.len >> 6;
-    uint32_t cur[16], nxt[16];
+    uint32_t cur[16];
     if (k0 < nfull) load_block16(en.p + 64ull * k0, cur);
     for (uint32_t k = k0; k < nfull; ++k) {
-        if (k + 1 < nfull) load_block16(en.p + 64ull * (k + 1), nxt);
+        // swap into the schedule window first (other registers), then
+        // refill `cur` with the next block in flight during the compression
         uint32_t w[16];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) w[j] = bswap(cur[j]);
+        for (int j = 0; j < 16; ++j) w[j] = bswap_fresh(cur[j]);
+        if (k + 1 < nfull) load_block16(en.p + 64ull * (k + 1), cur);
         compress(h, w);
-#pragma unroll
-        for (int j = 0; j < 16; ++j) cur[j] = nxt[j];
     }
 }
 
