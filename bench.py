@@ -75,14 +75,15 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 #    "vector-instruction ISSUE cost" row of MI355X_MICROARCH.md).  The floor
 #    is one chunk's serial chain: blocks x instructions x 4 cycles.
 #  * fused kernel (more groups): the SIMD's VALU time.  The fused loop issues
-#    621.75 VALU per block per wave of 64 chunks, and a SIMD completes about
+#    613.75 VALU per block per wave of 64 chunks (621.75 before round 4's
+#    fresh-register byte swap), and a SIMD completes about
 #    one VALU instruction every 4 cycles whatever its class: the PMC passes at
 #    131072 chunks (2 waves per SIMD) give 4.17 cycles per VALU per SIMD at the
 #    clock the chip holds, and 4 waves per SIMD take the same time per wave
 #    (profiles/pmc_shape_r03.json).  The round-2 model
 #    of 2 cycles for the "full-rate" ops (2043.5 cycles per block) is not
 #    reached by any kernel or microbenchmark here, so the ceiling below uses
-#    4 cycles per VALU: 2487 SIMD cycles per wave-block.
+#    4 cycles per VALU: 2455 SIMD cycles per wave-block.
 # Measured counterpart: the same compression on register data with no
 # memory traffic, every SIMD holding 8 waves, reaches 3940 GB/s of message
 # bytes (tools/microbench.hip compress_test "512 x 1024",
@@ -90,7 +91,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 COMPRESS_ONLY_GBS = 3939.8
 CONSUMER_INSTR_PER_BLOCK = 427.75
 ROUND_VALU_PER_BLOCK = 400
-FUSED_VALU_PER_BLOCK = 621.75
+FUSED_VALU_PER_BLOCK = 613.75  # tools/isa_mix.py, profiles/fused_vmov_r04.json
 FUSED_SIMD_CYCLES_PER_BLOCK = FUSED_VALU_PER_BLOCK * 4.0
 ISSUE_CYCLES = 4.0
 CLOCK_HZ = 2.4e9  # MI355X max engine clock; the chip holds it at config-2 occupancy
@@ -322,7 +323,7 @@ def main():
             "achieved": round(achieved, 2), "peak": round(valu_peak, 1), "unit": "GB/s",
             "frac": round(achieved / valu_peak, 4),
             "model": f"{cus * SIMDS_PER_CU} SIMDs x 64 chunks x 64 B per "
-                     f"{FUSED_SIMD_CYCLES_PER_BLOCK:g} SIMD cycles (621.75 VALU x 4) at 2.4 GHz",
+                     f"{FUSED_SIMD_CYCLES_PER_BLOCK:g} SIMD cycles ({FUSED_VALU_PER_BLOCK:g} VALU x 4) at 2.4 GHz",
             "measured_compress_only": COMPRESS_ONLY_GBS,
             "frac_of_measured": round(achieved / COMPRESS_ONLY_GBS, 4),
         },
