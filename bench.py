@@ -336,12 +336,21 @@ def main():
         result["strong"] = _strong_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden)
     if a.weak4_chunks > 0:
         result["weak_config4"] = _weak4_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden)
+    if rank == 0 and world == 1 and a.strong_total == 262144 and not a.no_configs:
+        # the per-GPU shards of the 1->8 strong curve that one GPU can time
+        # (VERDICT r4 next #1): N = 8 (32768 chunks, two groups of 64 per
+        # CU, the 8-wave split shape) and N = 2 (131072); N = 4's shard
+        # (65536) is weak_config4's workload
+        result["config4_shard8"] = _shard_leg(pkg, shard, torch, golden, 8, 1, a)
+        result["config4_shard2"] = _shard_leg(pkg, shard, torch, golden, 2, 1, a)
+        result["strong_projection"] = _strong_projection(result)
     if rank == 0 and world == 1 and not a.no_configs:
         # the other BASELINE configs on this GPU, each checked against the
         # reference's golden digests (configs 1, 3, 5; 2 and 4 are above)
         result["config5"] = _config5_leg(pkg, torch, golden)
         result["config3_e2e"] = _config3_leg(pkg, torch, golden)
         result["config1"] = _config1_leg(golden)
+        result["verify_queue"] = _verify_queue_leg(result["config3_e2e"].get("pinned_h2d_GiBps"))
     if rank == 0 and world == 1 and not a.no_latency:
         result["latency_one_chunk"] = _latency_one_chunk(dev)
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -355,7 +364,7 @@ def main():
             result["cpu_baseline"]["config1_reference_cli"] = ref
             c1 = result["config1"]
             c1["reference_cli_median_ms"] = ref["median_ms"]
-            for k in ("device", "host_small"):
+            for k in ("default", "device", "host_small"):
                 c1[k]["vs_reference"] = round(c1[k]["median_ms"] / ref["median_ms"], 3)
     if use_pg:
         result["config"]["control_plane"] = f"torch.distributed {backend}, world {world}"
@@ -429,6 +438,66 @@ def _strong_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden):
                                one_parity, K)
 
 
+def _shard_leg(pkg, shard, torch, golden, k, r, a) -> dict:
+    """Shard r of the k-way contiguous split of config 4's 262144-chunk list
+    (shard.strong_shard), hashed on this GPU: the per-GPU work of the strong
+    curve at N = k.  Timed like `strong` (3 untimed launches, then K),
+    checked against the reference golden shard aggregate, with the kernel's
+    issue floor for its regime."""
+    total, L, K = a.strong_total, CHUNK_LEN, max(1, a.strong_steps)
+    first, cnt = shard.strong_shard(r, k, total)
+    st = torch.cuda.Stream()
+    buf = torch.empty(cnt * L, dtype=torch.uint8, device="cuda")
+    dig = torch.zeros((cnt, 20), dtype=torch.uint8, device="cuda")
+    pkg.synth_fill_device(buf, first, cnt, L, stream=st)
+    torch.cuda.synchronize()
+    wall, kern_ms = _time_launches(pkg, torch, buf, L, cnt, dig, st, K, 3)
+    ok = hashlib.sha1(dig.cpu().numpy().tobytes()).hexdigest() == golden["config4"]["shard_aggs"][str(k)][r]
+    del buf, dig
+    torch.cuda.empty_cache()
+    cus = torch.cuda.get_device_properties(torch.cuda.current_device()).multi_processor_count
+    regime = _regime(cnt, cus, "auto")
+    blocks = (L + 8) // 64 + 1
+    out = {"workload": f"shard {r} of the {k}-way split of BASELINE config 4 ({cnt} x {L} B, "
+                       f"chunks {first}..{first + cnt - 1}), device-resident, one GPU",
+           "chunks": cnt, "steps": K, "ms_per_step": round(wall / K * 1e3, 4), "kernel_ms": round(kern_ms, 4),
+           "GiBps": round(cnt * L / (kern_ms * 1e-3) / 2**30, 2),
+           "hbm_frac": round(cnt * (L + 20) / (kern_ms * 1e-3) / (HBM_PEAK_GBS * 1e9), 5),
+           "kernel": regime, "parity": bool(ok),
+           "parity_ref": f"digest-of-digests == golden config4.shard_aggs[{k}][{r}] (reference sha.c)"}
+    if regime.startswith("split"):
+        floor = blocks * CONSUMER_INSTR_PER_BLOCK * ISSUE_CYCLES / CLOCK_HZ * 1e3
+        out["floor_ms"] = round(floor, 4)
+        out["floor_frac"] = round(floor / kern_ms, 4)
+        out["floor_model"] = (f"one chunk's serial chain: {blocks} blocks x {CONSUMER_INSTR_PER_BLOCK} "
+                              f"consumer instructions x {ISSUE_CYCLES:g} cyc / 2.4 GHz")
+    else:
+        waves_per_simd = (cnt + 63) // 64 / (cus * SIMDS_PER_CU)
+        floor = waves_per_simd * blocks * FUSED_SIMD_CYCLES_PER_BLOCK / CLOCK_HZ * 1e3
+        out["floor_ms"] = round(floor, 4)
+        out["floor_frac"] = round(floor / kern_ms, 4)
+        out["floor_model"] = f"SIMD VALU issue: {waves_per_simd:g} waves/SIMD x {blocks} blocks x " \
+                             f"{FUSED_SIMD_CYCLES_PER_BLOCK:g} cyc / 2.4 GHz"
+    return out
+
+
+def _strong_projection(result) -> dict:
+    """Config 4's strong curve as one GPU predicts it: the shards are equal
+    and independent (no collective), so N GPUs take as long as one GPU takes
+    for its 262144/N-chunk shard.  Speed-up = the whole list's kernel time
+    (`strong`, N = 1) / the shard's."""
+    one = result.get("strong", {}).get("one_gpu_kernel_ms")
+    shards = {"2": result.get("config4_shard2"), "4": result.get("weak_config4"),
+              "8": result.get("config4_shard8")}
+    out = {"basis": "one-GPU kernel time of the whole 262144-chunk list / of one shard "
+                    "(N = 4: weak_config4, whose 65536 chunks are one shard of the 4-way split)"}
+    if one:
+        out["speedup"] = {n: round(one / v["kernel_ms"], 3) for n, v in shards.items() if v and v.get("kernel_ms")}
+        out["efficiency"] = {n: round(x / int(n), 4) for n, x in out["speedup"].items()}
+    out["parity"] = all(v.get("parity", False) for v in shards.values() if v)
+    return out
+
+
 def _weak4_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden):
     """Config 4's weak scaling (65536 chunks per GPU): every
     rank hashes its own `per` chunks, no collective on the data path.  Rank r
@@ -472,11 +541,12 @@ def _weak4_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden):
 
 def _latency_one_chunk(dev: int) -> dict:
     """verify_hash (job.c:217-228) on one 512 KiB chunk through the library in
-    a child process: the first call (HIP start-up and stream creation
-    included) and the median of 20 warm calls; then the same with the
-    opt-in host small-call path (SHA1CHUNK_HOST_SMALL=524288: the chunk is
-    hashed on the host, csrc/sha1_host.c, the device still required -- and
-    checked through the KFD topology, so no HIP start-up either)."""
+    a child process: the first call (library load included) and the median
+    of 20 warm calls, with the library's default routing (one message on the
+    host: csrc/sha1_host.c, the device still required and checked through
+    the KFD topology, so no HIP start-up) and on the kernels
+    (SHA1CHUNK_HOST_SMALL=0: one lane's serial chain, HIP start-up in the
+    first call)."""
     import subprocess
     code = (
         "import ctypes, hashlib, json, os, sys, time\n"
@@ -504,7 +574,7 @@ def _latency_one_chunk(dev: int) -> dict:
     libp = os.path.join(ROOT, "congestion-control-with-bittorren_amd", "libsha1chunk.so")
 
     def child(extra_env):
-        env = dict(os.environ, **extra_env)
+        env = _env_without_knob(extra_env)
         r = subprocess.run([sys.executable, "-c", code, libp, str(dev)], capture_output=True,
                            text=True, timeout=120, env=env)
         line = [x for x in r.stdout.splitlines() if x.startswith("LATENCY ")]
@@ -514,21 +584,21 @@ def _latency_one_chunk(dev: int) -> dict:
 
     try:
         d = child({})
-        hs = child({"SHA1CHUNK_HOST_SMALL": str(CHUNK_LEN)})
+        dv = child({"SHA1CHUNK_HOST_SMALL": "0"})
     except Exception as e:  # a failed probe must not cost the bench line
         return {"error": repr(e)[:300]}
-    return {"path": "verify_hash -> get_chunk_hash -> shahash -> sha1chunk_hash_batch(n=1): "
-                    "one lane of the split kernel (job.c:217-228)",
+    return {"path": "verify_hash -> get_chunk_hash -> shahash (job.c:217-228), the library's default "
+                    "routing: one message is hashed on the host (csrc/sha1_host.c, x86 SHA extensions; "
+                    "a gfx950 device is still required, checked through the KFD topology)",
             "cold_ms": round(d["probe_ms"] + d["first_call_ms"], 3),
             "cold_first_call_ms": round(d["first_call_ms"], 3),
             "warm_ms": round(d["warm_ms"], 3), "warm_min_ms": round(d["warm_min_ms"], 3),
             "bytes": CHUNK_LEN,
-            "host_small": {"knob": f"SHA1CHUNK_HOST_SMALL={CHUNK_LEN} (opt-in; off by default)",
-                           "path": "shahash on the host (csrc/sha1_host.c, x86 SHA extensions); "
-                                   "a device is still required",
-                           "cold_ms": round(hs["probe_ms"] + hs["first_call_ms"], 3),
-                           "cold_first_call_ms": round(hs["first_call_ms"], 3),
-                           "warm_ms": round(hs["warm_ms"], 3), "warm_min_ms": round(hs["warm_min_ms"], 3)}}
+            "device": {"knob": "SHA1CHUNK_HOST_SMALL=0 (every call on the kernels)",
+                       "path": "shahash -> sha1chunk_hash_batch(n=1): one lane of the split kernel",
+                       "cold_ms": round(dv["probe_ms"] + dv["first_call_ms"], 3),
+                       "cold_first_call_ms": round(dv["first_call_ms"], 3),
+                       "warm_ms": round(dv["warm_ms"], 3), "warm_min_ms": round(dv["warm_min_ms"], 3)}}
 
 
 class _CaptureStderr:
@@ -743,10 +813,55 @@ def _config3_leg(pkg, torch, golden, reps: int = 2) -> dict:
             "parity_ref": "digest-of-digests == golden config3.agg (reference sha.c)"}
 
 
+def _verify_queue_leg(h2d_gibps) -> dict:
+    """SURVEY 8(f) rank 2, the received-chunk verify queue (reliable_udp.c:121
+    session buffer, filled at :339; packet_handler.c:472 -> job.c:217-228):
+    16384 x 512 KiB host chunks, reassembled by 4 receive threads in 1484-byte
+    DATA payloads, 20 % corrupted in place before the verify, through
+    tools/vq_zc_bench (C, linked against libsha1chunk.so): zero-copy
+    (sha1chunk_vq_reserve / commit / release) and the reference's own call
+    shape (fill a malloc'd session buffer, sha1chunk_vq_submit).  Every result
+    is checked against the verdict the reference golden digests give
+    (tests/golden/synth_4096x512k.bin); GiB/s next to this run's pinned H2D."""
+    import subprocess
+    tool = os.path.join(ROOT, "tools", "vq_zc_bench")
+    out = {"workload": "16384 x 524288 B host chunks, 4 receive threads filling 1484-byte pieces, "
+                       "20 % corrupted, persistent drain", "pinned_h2d_GiBps": h2d_gibps}
+    if not os.path.exists(tool):
+        out["error"] = "tools/vq_zc_bench not built (make -C congestion-control-with-bittorren_amd tools)"
+        return out
+    for mode in ("reserve", "submit"):
+        try:
+            r = subprocess.run([tool, "--mode", mode, "--chunks", "16384", "--producers", "4",
+                                "--distinct", "4096", "--pieces", "1",
+                                "--golden", os.path.join(ROOT, "tests/golden/synth_4096x512k.bin")],
+                               capture_output=True, text=True, timeout=180, cwd=ROOT)
+            line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+            rec = json.loads(line[-1]) if line else {"error": (r.stderr or r.stdout)[-300:]}
+        except Exception as e:  # a failed leg must not cost the bench line
+            rec = {"error": repr(e)[:300]}
+        if "GiBps" in rec:
+            rec["parity"] = bool(rec.get("results_correct")) and rec.get("flagged") == len(range(2, 16384, 5))
+            if h2d_gibps:
+                rec["over_h2d"] = round(rec["GiBps"] / h2d_gibps, 4)
+        out["zero_copy" if mode == "reserve" else "submit"] = rec
+    out["parity"] = all(out.get(k, {}).get("parity", False) for k in ("zero_copy", "submit"))
+    out["parity_ref"] = "every chunk's 0/1 == (its bytes hash to the reference golden digest); 3277 flagged"
+    return out
+
+
+def _env_without_knob(extra=None) -> dict:
+    """The environment with the library's default routing (no
+    SHA1CHUNK_HOST_SMALL), plus `extra`."""
+    env = {k: v for k, v in os.environ.items() if k != "SHA1CHUNK_HOST_SMALL"}
+    env.update(extra or {})
+    return env
+
+
 def _run_cli(argv, env_extra, reps):
     """Whole-process wall times (s) of `reps` runs of a CLI, and its stdout."""
     import subprocess
-    env = dict(os.environ, **env_extra)
+    env = _env_without_knob(env_extra)
     ts, out = [], None
     for _ in range(reps):
         t0 = time.perf_counter()
@@ -776,21 +891,25 @@ def _ctar_file() -> str:
 def _config1_leg(golden, reps: int = 7) -> dict:
     """BASELINE config 1: `make-chunks tmp/C.tar` (make_chunks.c:14-62 ->
     chunk.c:15-27), the repo's CLI as a whole process, first run and median
-    of the rest: the default device path and the opt-in host small-file path
-    (SHA1CHUNK_HOST_SMALL).  Output must equal the reference's tmp/C.chunks
-    (CRLF stripped).  The reference's own CLI is timed in cpu_baseline."""
+    of the rest: the library's default routing (a regular file of <= 4 MiB
+    is hashed on the host, csrc/frontend.c), the kernels
+    (SHA1CHUNK_HOST_SMALL=0) and the explicit knob at the file's size.
+    Output must equal the reference's tmp/C.chunks (CRLF stripped).  The
+    reference's own CLI is timed in cpu_baseline."""
     path = _ctar_file()
     cli = os.path.join(ROOT, "congestion-control-with-bittorren_amd", "make-chunks")
     res = {"workload": "BASELINE config 1: make-chunks tmp/C.tar (2 MiB, 4 chunks), whole process",
            "file_bytes": os.path.getsize(path)}
     try:
-        for name, env in (("device", {}),
+        for name, env in (("default", {}), ("device", {"SHA1CHUNK_HOST_SMALL": "0"}),
                           ("host_small", {"SHA1CHUNK_HOST_SMALL": str(os.path.getsize(path))})):
             ts, out = _run_cli([cli, path], env, reps)
             res[name] = {"first_ms": round(ts[0] * 1e3, 3),
                          "median_ms": round(float(np.median(ts[1:])) * 1e3, 3),
                          "parity": _cli_rows_ok(out, golden)}
-        res["parity"] = res["device"]["parity"] and res["host_small"]["parity"]
+        res["default"]["route"] = "host (regular file <= 4 MiB, the library's default)"
+        res["device"]["route"] = "gfx950 kernels (SHA1CHUNK_HOST_SMALL=0)"
+        res["parity"] = all(res[k]["parity"] for k in ("default", "device", "host_small"))
     finally:
         os.unlink(path)
     return res

@@ -11,9 +11,15 @@
  *   verify_chunk_hash                   chunk.c:204-217
  *   verify_hash                         job.c:217-228
  *
- * Every SHA-1 compression goes to the device (unless the process opts into
- * SHA1CHUNK_HOST_SMALL, which hashes calls up to that size on the host and
- * still requires the device; sha1_runtime.hip, sha1_host.c).  The reference
+ * Routing (frontend.c, SHA1CHUNK_HOST_SMALL): the single-message calls --
+ * shahash and what is built on it (get_chunk_hash, verify_hash, the per-call
+ * verify_chunk_hash), the SHA1Update/SHA1Final trio -- and make_chunks on a
+ * regular file of at most 4 MiB hash on the host by default (sha1_host.c;
+ * SURVEY.md 7.1 step 2, 8(b)), since one message is one serial chain that a
+ * GPU lane runs ~30x slower than a CPU core; make_chunks on larger files and
+ * streams, and the master-file index, run on the gfx950 kernels
+ * (sha1_runtime.hip), as everything does under SHA1CHUNK_HOST_SMALL=0.  A
+ * device is required either way.  The reference
  * reports failures by printing and exit(-1) (chunk.c:171-178); these void
  * functions do the same when the engine fails (no device, HIP error), so a
  * missing GPU is loud, never a silent CPU fallback.
@@ -30,6 +36,7 @@
 #include "../../include/chunk_hash.h"
 #include "../../include/sha.h"
 #include "../../include/sha1chunk.h"
+#include "frontend.h"
 
 #define CHUNK_LEN 524288 /* constants.h:14 */
 
@@ -107,9 +114,7 @@ void shahash(uint8_t *str, int len, uint8_t *hash) {
         fprintf(stderr, "sha1chunk: shahash: negative length %d\n", len);
         exit(-1);
     }
-    const uint64_t off = 0;
-    const uint32_t n = (uint32_t)len;
-    check("shahash", sha1chunk_hash_batch(str, &off, &n, 1, hash, SHA1CHUNK_HOST));
+    check("shahash", sha1chunk_digest(str, (uint64_t)len, hash));
 }
 
 void binary2hex(uint8_t *buf, int len, char *hex) {
@@ -288,6 +293,7 @@ static int master_lookup(FILE *f, size_t idx, uint8_t out20[20], off_t *size) {
     struct stat st;
     int fd = fileno(f);
     if (fd < 0 || fstat(fd, &st) || !S_ISREG(st.st_mode) || st.st_size <= 0) return 0;
+    if (fe_file_on_host((uint64_t)st.st_size)) return 0; /* small file: per-call host hash */
     if (!settled(&st)) return 0; /* changed just now: re-read and re-hash */
     file_key k = {st.st_dev, st.st_ino, st.st_size, st.st_mtim, st.st_ctim};
     int hit = 0;

@@ -7,16 +7,17 @@
  * alone.  Every call that reaches the GPU is forwarded to the HIP backend,
  * libsha1chunk_hip.so (sha1_runtime.hip + the gfx950 kernels), which this
  * file dlopen()s from its own directory on the first such call -- so a
- * process that only makes small host calls (SHA1CHUNK_HOST_SMALL, below)
- * never loads the HIP runtime: loading libamdhip64 costs ~11 ms and starting
- * it 50-250 ms (profiles/startup_r03.json), against the 6.5 ms the
- * reference's whole make-chunks takes on tmp/C.tar (BASELINE config 1).
+ * process that only makes single-message host calls (below) never loads the
+ * HIP runtime: loading libamdhip64 costs ~11 ms and starting it 50-250 ms
+ * (profiles/startup_r03.json), against the 6.5 ms the reference's whole
+ * make-chunks takes on tmp/C.tar (BASELINE config 1).
  *
  * What the front end does itself:
- *   - the opt-in host small-call path (SHA1CHUNK_HOST_SMALL=<bytes>): host
- *     batches, the streaming trio's compressions and final, make_chunks on a
- *     regular file, and the batch-1 verify queue of at most that many bytes
- *     are hashed here by sha1_host.c (x86 SHA extensions);
+ *   - the host path (sha1_host.c, x86 SHA extensions) for the reference's
+ *     single-message calls by default -- shahash and its callers, the
+ *     streaming trio, make_chunks on a regular file of at most 4 MiB -- and,
+ *     under SHA1CHUNK_HOST_SMALL=<bytes>, for host batches and the batch-1
+ *     verify queue of at most that many bytes (routing rules below);
  *   - the device check of those paths, without starting HIP: the kernel
  *     driver's KFD topology must list an accessible gfx950 agent
  *     (light_count);
@@ -38,9 +39,11 @@
 #include <unistd.h>
 
 #include "../../include/sha1chunk.h"
+#include "frontend.h"
 #include "sha1_host.h"
 
 #define FE_API __attribute__((visibility("default")))
+#define FE_HIDDEN __attribute__((visibility("hidden")))
 
 static __thread char t_err[512];
 static __thread int t_dev = 0;       /* this thread's device (sha1chunk_set_device) */
@@ -122,7 +125,7 @@ static void be_load(void) {
         return;                                                                                   \
     }
     BACKEND_FUNCS(BE_SYM)
-    be_ok = 1;
+    __atomic_store_n(&be_ok, 1, __ATOMIC_RELEASE); /* read without the once by set_device */
 }
 
 /* The backend, loaded; 0 or a negative error. */
@@ -154,16 +157,48 @@ static int backend_dev(void) {
     } while (0)
 
 /* --------------------------------------------------- host small-call path -- */
+/* SHA1CHUNK_HOST_SMALL, read once per process, routes the calls that hash on
+ * the host (sha1_host.c; a device is required either way, require_device):
+ *
+ *   unset      the default ("shahash() /
+ *              verify_hash() keep a CPU path", "the streaming trio stays
+ *              CPU"): the reference's synchronous single-message calls --
+ *              shahash, get_chunk_hash, verify_hash, verify_chunk_hash's
+ *              per-call path, and the SHA1Update / SHA1Final trio
+ *              (sha1chunk_compress_blocks / sha1chunk_finish) -- are hashed
+ *              on the host at any length, and make_chunks /
+ *              sha1chunk_hash_fd on a regular file of at most REF_FILE_BYTES.
+ *              One message is one serial chain: a lane of the GPU hashes it
+ *              at ~85 MB/s, a CPU core at ~2.5 GB/s.  Every batch, device and
+ *              verify-queue call runs on the kernels.
+ *   "0"        every call on the kernels (the GPU tests pin this).
+ *   "<bytes>"  the opt-in of rounds 3-4: every host call of at most that
+ *              many bytes on the host -- batches, the trio, a regular file,
+ *              a verify queue of batch 1 whose max length fits -- and larger
+ *              ones on the kernels. */
+#define REF_FILE_BYTES (4ull << 20) /* make-chunks on tmp/C.tar (2 MiB), BASELINE config 1 */
 static uint64_t g_small;
+static int g_small_set;
 static pthread_once_t small_once = PTHREAD_ONCE_INIT;
 static void small_init(void) {
     const char *e = getenv("SHA1CHUNK_HOST_SMALL");
-    g_small = e ? strtoull(e, NULL, 10) : 0ull;
+    g_small_set = e != NULL && *e != 0;
+    g_small = g_small_set ? strtoull(e, NULL, 10) : 0ull;
 }
-/* SHA1CHUNK_HOST_SMALL=<bytes> (default 0: off), read once per process. */
+/* The explicit knob's byte count (0 when unset or "0"): batches and queues. */
 static uint64_t host_small_bytes(void) {
     pthread_once(&small_once, small_init);
     return g_small;
+}
+/* 1 when a single-message reference call of `bytes` bytes hashes on the host. */
+static int ref_on_host(uint64_t bytes) {
+    pthread_once(&small_once, small_init);
+    return g_small_set ? g_small != 0 && bytes <= g_small : 1;
+}
+/* 1 when make_chunks on a regular file of `bytes` bytes hashes on the host. */
+static int file_on_host(uint64_t bytes) {
+    pthread_once(&small_once, small_init);
+    return g_small_set ? g_small != 0 && bytes <= g_small : bytes <= REF_FILE_BYTES;
 }
 
 /* Presence check of the host small-call paths without starting HIP: the KFD
@@ -304,7 +339,7 @@ FE_API int sha1chunk_set_device(int device) {
     /* With the backend loaded it validates against the HIP probe; before
      * that, against the KFD check (a host-only process stays HIP-free), and
      * the backend validates again at the first forwarded call. */
-    const int lc = be_ok ? -1 : light_count();
+    const int lc = __atomic_load_n(&be_ok, __ATOMIC_ACQUIRE) ? -1 : light_count();
     if (lc < 0) {
         int rc = backend();
         if (rc) return rc;
@@ -369,6 +404,26 @@ FE_API int sha1chunk_verify_batch(const void *base, const uint64_t *offsets, con
     FORWARD(int, verify_batch(base, offsets, lengths, n, expected, mismatch, flags));
 }
 
+/* One message (shahash, chunk.c:35-51, and the calls built on it), routed
+ * like the other single-message reference calls (ref_on_host). */
+FE_API int sha1chunk_digest(const void *msg, uint64_t len, uint8_t digest[20]) {
+    if ((len && !msg) || !digest) return fail(SHA1CHUNK_EINVAL, "null pointer");
+    if (ref_on_host(len)) {
+        int rc = require_device();
+        if (rc) return rc;
+        sha1host_digest(msg, len, digest);
+        return SHA1CHUNK_OK;
+    }
+    if (len > 0xffffffffull) return fail(SHA1CHUNK_EINVAL, "a message above 4 GiB - 1 on the kernels");
+    const uint64_t off = 0;
+    const uint32_t n = (uint32_t)len;
+    FORWARD(int, hash_batch(len ? msg : digest, &off, &n, 1, digest, SHA1CHUNK_HOST));
+}
+
+/* make_chunks's master-file index (chunk_api.c): a device pass over the
+ * whole file pays off only where make_chunks itself would use the device. */
+FE_HIDDEN int fe_file_on_host(uint64_t bytes) { return file_on_host(bytes); }
+
 FE_API int sha1chunk_hash_device_async(const void *d_base, const uint64_t *d_offsets,
                                        const uint32_t *d_lengths, size_t n, uint8_t *d_digests,
                                        void *stream, int kernel) {
@@ -430,11 +485,10 @@ static long hash_file_host(int fd, off_t pos, off_t end, uint8_t *digests, size_
 }
 
 FE_API long sha1chunk_hash_fd(int fd, uint8_t *digests, size_t max_chunks, size_t *total_chunks) {
-    const uint64_t small = host_small_bytes();
     struct stat st;
     const off_t pos = lseek(fd, 0, SEEK_CUR);
-    if (small && pos >= 0 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode) &&
-        (uint64_t)(st.st_size > pos ? st.st_size - pos : 0) <= small) {
+    if (pos >= 0 && fstat(fd, &st) == 0 && S_ISREG(st.st_mode) &&
+        file_on_host((uint64_t)(st.st_size > pos ? st.st_size - pos : 0))) {
         int rc = require_device();
         if (rc) return rc;
         const long n = hash_file_host(fd, pos, st.st_size > pos ? st.st_size : pos, digests, max_chunks);
@@ -449,7 +503,7 @@ FE_API int sha1chunk_compress_blocks(uint32_t state[5], const void *blocks, size
     if (!state || (nblocks && !blocks)) return fail(SHA1CHUNK_EINVAL, "null pointer");
     if (nblocks == 0) return SHA1CHUNK_OK;
     if (nblocks * 64 > 0xffffffffull) return fail(SHA1CHUNK_EINVAL, "too many blocks");
-    if (nblocks * 64 <= host_small_bytes()) {
+    if (ref_on_host(nblocks * 64)) {
         int rc = require_device();
         if (rc) return rc;
         sha1host_compress(state, blocks, nblocks);
@@ -462,7 +516,7 @@ FE_API int sha1chunk_finish(const uint32_t state[5], uint64_t prefix_bytes, cons
                             uint32_t tail_len, uint8_t digest[20]) {
     if (!state || !digest || (tail_len && !tail) || tail_len >= 64)
         return fail(SHA1CHUNK_EINVAL, "bad argument");
-    if (host_small_bytes()) {
+    if (ref_on_host(tail_len)) {
         int rc = require_device();
         if (rc) return rc;
         sha1host_finish(state, prefix_bytes, tail, tail_len, digest);

@@ -58,7 +58,7 @@ struct VqDrainArgs {
     const uint32_t* grp;     // host: per group ring entry {first slot, count}
     const uint32_t* pub;     // host: groups published so far
     const uint32_t* stop;    // host: nonzero = exit once nothing is claimable
-    uint32_t* alive;         // host: per workgroup, 1 while it may still claim
+    uint8_t* alive;          // host: per workgroup, 1 while it may still claim
     uint8_t* res;            // host: per slot, 0 match / 1 mismatch
     uint32_t* done;          // host: per group ring entry, group index + 1 when done
     uint32_t* last_done;     // host: the last group finished (index + 1), any order

@@ -227,6 +227,10 @@ __device__ __forceinline__ uint32_t ld_sys(const uint32_t* p) {
 __device__ __forceinline__ void st_sys(uint32_t* p, uint32_t v) {
     __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
+// alive flags are bytes: the host reads 16 workgroups' flags per uncached load
+__device__ __forceinline__ void st_sys(uint8_t* p, uint8_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
 
 // Lane 0 only: a claimed group index, kVqIdle or kVqExit.  Idleness is the
 // queue's, not the workgroup's: `last` is when the claim counter last moved
@@ -240,7 +244,7 @@ __device__ uint32_t vq_next(const VqDrainArgs& Q, uint64_t& last, uint32_t& seen
     // leaves between groups, work pending or not; the host relaunches the
     // drain on its next call (pvq_ensure_drain counts the live workgroups).
     if (__builtin_amdgcn_s_memrealtime() - born > Q.life_ticks) {
-        st_sys(Q.alive + blockIdx.x, 0u);
+        st_sys(Q.alive + blockIdx.x, uint8_t{0});
         return kVqExit;
     }
     for (int round = 0; round < 2; ++round) {
@@ -261,10 +265,10 @@ __device__ uint32_t vq_next(const VqDrainArgs& Q, uint64_t& last, uint32_t& seen
         if (ld_sys(Q.stop)) return kVqExit;
         if (round == 1 || __builtin_amdgcn_s_memrealtime() - last <= Q.idle_ticks) return kVqIdle;
         // idle too long: leave, unless a group was published meanwhile
-        st_sys(Q.alive + blockIdx.x, 0u);
+        st_sys(Q.alive + blockIdx.x, uint8_t{0});
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
         if (__hip_atomic_load(Q.claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= ld_sys(Q.pub)) return kVqExit;
-        st_sys(Q.alive + blockIdx.x, 1u);
+        st_sys(Q.alive + blockIdx.x, uint8_t{1});
         __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "");
     }
     return kVqIdle;

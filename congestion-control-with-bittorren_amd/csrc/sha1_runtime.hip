@@ -1310,7 +1310,7 @@ struct PvqCtl {
     uint32_t stop;       // destroy: exit once nothing is claimable
     uint32_t last_done;  // drain: index + 1 of the group it finished last
     uint32_t pad[29];
-    uint32_t alive[2][1024];  // per launch slot, per workgroup
+    uint8_t alive[2][1024];   // per launch slot, per workgroup (bytes: 16 per uncached read)
 };
 struct PvqGroup {
     uint64_t g;         // group index
@@ -1325,6 +1325,7 @@ struct PvqRegion {
     bool committed;  // a slot refers to it: its result is pending until collected
     bool collected;
     bool released;
+    std::thread::id owner;  // the thread that allocated it (reserve or submit)
 };
 struct Pvq {
     int dev = 0, cus = 256;  // cus: the drain's workgroups (one per CU)
@@ -1400,7 +1401,7 @@ uint64_t env_u64(const char* name, uint64_t dflt) {
 int pvq_launch(Pvq* P, int k, int wgs) {
     // every workgroup of the new drain counts as alive from here on, so a
     // submit right after does not launch another one
-    for (int w = 0; w < wgs; ++w) __atomic_store_n(&P->ctl->alive[k][w], 1u, __ATOMIC_RELEASE);
+    for (int w = 0; w < wgs; ++w) __atomic_store_n(&P->ctl->alive[k][w], uint8_t{1}, __ATOMIC_RELEASE);
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
     VqDrainArgs Q{};
     Q.data = P->dma ? P->ddata : P->data;
@@ -1438,11 +1439,17 @@ int pvq_launch(Pvq* P, int k, int wgs) {
 // workgroups are alive, the missing ones are launched on a slot whose
 // previous drain has ended; the leftovers of the old one keep working.
 //
-// The alive words are uncached host memory (a CPU read costs ~0.15 us, and
+// The alive flags are uncached host memory (a CPU read costs ~0.15 us, and
 // every submit, commit and poll lands here under the queue's lock), so they
-// are read 16 bytes at a time, and not again within kAliveScanNs of a scan
-// that found the drain at full strength: a workgroup that leaves in that
-// window is replaced at most that much later (workgroups live >= 4 ms).
+// are bytes read 16 at a time -- 8 reads for a 64-workgroup drain's two
+// launch slots -- and a call that did not move `pub` does not read them again
+// within kAliveScanNs of a scan that found the drain at full strength: a
+// workgroup that leaves in that window is replaced at most that much later
+// (workgroups live >= 4 ms), and the next publish rescans anyway.  A call
+// that moved `pub` (publish, or a DMA-staged group released) always reads
+// them: that read is the host's half of the exit handshake, so
+// a group published just as the drain's last workgroups leave is never left
+// unclaimed until some later call.
 constexpr int64_t kAliveScanNs = 50000;
 
 int64_t mono_ns() {
@@ -1451,21 +1458,23 @@ int64_t mono_ns() {
     return int64_t(ts.tv_sec) * 1000000000 + ts.tv_nsec;
 }
 
-int count_alive(const uint32_t* a, int n) {
+int count_alive(const uint8_t* a, int n) {
     int c = 0, w = 0;
-    for (; w + 4 <= n; w += 4) {  // one 16-byte uncached read per 4 words
+    for (; w + 16 <= n; w += 16) {  // one 16-byte uncached read per 16 flags
         const __m128i v = _mm_load_si128(reinterpret_cast<const __m128i*>(a + w));
-        c += 4 - __builtin_popcount(_mm_movemask_ps(_mm_castsi128_ps(_mm_cmpeq_epi32(v, _mm_setzero_si128()))));
+        c += 16 - __builtin_popcount(_mm_movemask_epi8(_mm_cmpeq_epi8(v, _mm_setzero_si128())));
     }
     for (; w < n; ++w) c += __atomic_load_n(a + w, __ATOMIC_ACQUIRE) != 0;
     return c;
 }
 
-int pvq_ensure_drain(Pvq* P) {
+int pvq_ensure_drain(Pvq* P, bool moved_pub = false) {
     const int64_t now = mono_ns();
-    if (P->alive_seen >= P->cus && now - P->alive_scan_ns < kAliveScanNs) return SHA1CHUNK_OK;
+    if (!moved_pub && P->alive_seen >= P->cus && now - P->alive_scan_ns < kAliveScanNs) return SHA1CHUNK_OK;
     __atomic_thread_fence(__ATOMIC_SEQ_CST);
-    const int alive = count_alive(P->ctl->alive[0], P->cus) + count_alive(P->ctl->alive[1], P->cus);
+    int alive = 0;
+    for (int k = 0; k < 2; ++k)  // a slot never launched has no live workgroup
+        if (P->launched[k]) alive += count_alive(P->ctl->alive[k], P->cus);
     ++P->n_scans;
     __atomic_thread_fence(__ATOMIC_ACQUIRE);
     P->alive_scan_ns = now;
@@ -1496,7 +1505,7 @@ int pvq_release_staged(Pvq* P) {
         P->staged.pop_front();
         moved = true;
     }
-    return moved ? pvq_ensure_drain(P) : SHA1CHUNK_OK;
+    return moved ? pvq_ensure_drain(P, true) : SHA1CHUNK_OK;
 }
 
 // Copy the chunks of slots [slot0, slot0 + count) into the device ring and
@@ -1541,6 +1550,10 @@ int pvq_stage(Pvq* P, uint64_t g, uint64_t slot0, uint32_t count) {
 
 int pvq_publish(Pvq* P) {
     if (P->open_count == 0) return SHA1CHUNK_OK;
+    // the drain indexes a group's slots first..first+count with no modulo
+    if (P->open_slot0 % P->nslots + P->open_count > P->nslots || P->open_count > kPvqMaxGroup)
+        return fail(SHA1CHUNK_EHIP, "vq: internal: group of %u slots at %llu crosses the slot ring's end",
+                    P->open_count, static_cast<unsigned long long>(P->open_slot0 % P->nslots));
     const uint64_t g = P->next_g++;
     const uint32_t gi = static_cast<uint32_t>(g % P->nslots);
     P->grp[2 * gi] = static_cast<uint32_t>(P->open_slot0 % P->nslots);
@@ -1560,7 +1573,7 @@ int pvq_publish(Pvq* P) {
     }
     // the group's bytes, lengths, digests and descriptor are written: release them
     __atomic_store_n(&P->ctl->pub, static_cast<uint32_t>(g + 1), __ATOMIC_RELEASE);
-    return pvq_ensure_drain(P);
+    return pvq_ensure_drain(P, true);
 }
 
 // A region is free once nothing refers to it: a copied chunk once its
@@ -1641,7 +1654,9 @@ int pvq_wait(Pvq* P, Pred pred, const char* what, Stuck stuck) {
         if (pred()) return SHA1CHUNK_OK;
         if (P->open_count && (rc = pvq_publish(P))) return rc;
         if (stuck())
-            return fail(SHA1CHUNK_ENOMEM, "vq: %s: the ring is held by %zu reserved buffers not released",
+            return fail(SHA1CHUNK_ENOMEM,
+                        "vq: %s: the ring's oldest region is this thread's own reserved buffer, not committed "
+                        "or not released (%zu reserved buffers held)",
                         what, P->held.size());
         if (P->inflight && (rc = pvq_ensure_drain(P))) return rc;
         if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
@@ -1819,6 +1834,24 @@ unsigned ring_flags() {
     return e && !strcmp(e, "coherent") ? hipHostMallocCoherent : hipHostMallocUncached;
 }
 
+// The verify queue's own streams (its drains' two launch slots and its copy
+// stream) are created at a priority of their own (SHA1CHUNK_VQ_PRIO: "low",
+// the default, "normal" or "high").  HIP serves a process's streams from a
+// few hardware queues (GPU_MAX_HW_QUEUES, 4) and streams of different
+// priorities from different ones, so a queue's persistent drain and the
+// barrier packets its copy stream's events leave behind (each waits for a
+// staged copy on the copy engine) never sit in front of the caller's own
+// work -- a hash batch on a stream of the default priority.
+int vq_stream_create(hipStream_t* s) {
+    const char* e = getenv("SHA1CHUNK_VQ_PRIO");
+    const std::string want = e ? e : "low";
+    if (want == "normal") return hipStreamCreateWithFlags(s, hipStreamNonBlocking) == hipSuccess ? 0 : -1;
+    int least = 0, greatest = 0;
+    if (hipDeviceGetStreamPriorityRange(&least, &greatest) != hipSuccess) return -1;
+    const int prio = want == "high" ? greatest : least;
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, prio) == hipSuccess ? 0 : -1;
+}
+
 // The device's logical index for D (the CU budget lives there).
 int device_index(Device* D) { return static_cast<int>(D - g_dev); }
 
@@ -1856,7 +1889,7 @@ Pvq* pvq_create(Device* D, size_t batch, uint32_t max_chunk_len, int cus) {
     if (P->dma) {
         P->hdata_bytes = P->nbytes;
         if (!(P->hdata = ring_get(P->nbytes, hipHostMallocDefault)) || !(P->ddata = dring_get(P->dev, P->nbytes)) ||
-            hipStreamCreateWithFlags(&P->cstream, hipStreamNonBlocking) != hipSuccess) {
+            vq_stream_create(&P->cstream) != 0) {
             (void)hipGetLastError();
             fail(SHA1CHUNK_ENOMEM, "vq: DMA-staged ring of %llu bytes", static_cast<unsigned long long>(P->nbytes));
             pvq_destroy(P);
@@ -1879,7 +1912,7 @@ Pvq* pvq_create(Device* D, size_t batch, uint32_t max_chunk_len, int cus) {
     // order on stream 0, so creating a queue never waits for the whole device
     // (other threads' drains and batches)
     for (int k = 0; k < 2; ++k)
-        if (hipStreamCreateWithFlags(&P->stream[k], hipStreamNonBlocking) != hipSuccess ||
+        if (vq_stream_create(&P->stream[k]) != 0 ||
             hipEventCreateWithFlags(&P->ended[k], hipEventDisableTiming) != hipSuccess) {
             fail(SHA1CHUNK_EHIP, "vq: stream creation");
             pvq_destroy(P);
@@ -1919,15 +1952,21 @@ int pvq_alloc(Pvq* P, uint32_t len, bool reserved, uint64_t* id) {
         const uint64_t t = P->byte_tail;
         return (t % P->nbytes) + need > P->nbytes ? t + (P->nbytes - t % P->nbytes) : t;
     };
+    // Only the caller's own buffer at the ring's head makes the wait hopeless
+    // (this thread cannot commit or release it while it waits here); another
+    // thread's reservation there is a session still filling or not yet
+    // released, which that thread will commit or release, so the
+    // call waits for it as for any in-flight group (bounded, pvq_wait).
+    const std::thread::id me = std::this_thread::get_id();
     auto stuck = [&] {
         if (P->regions.empty()) return false;
         const PvqRegion& r = P->regions.front();
-        return r.reserved && !r.released && (!r.committed || r.collected);
+        return r.reserved && !r.released && (!r.committed || r.collected) && r.owner == me;
     };
     if (int rc = pvq_wait(P, [&] { return pos() + need - P->byte_head <= P->nbytes; }, "data ring full", stuck))
         return rc;
     const uint64_t at = pos();
-    P->regions.push_back(PvqRegion{at, at + need, reserved, false, false, false});
+    P->regions.push_back(PvqRegion{at, at + need, reserved, false, false, false, me});
     P->byte_tail = at + need;
     *id = P->reg_base + P->regions.size() - 1;
     return SHA1CHUNK_OK;
@@ -1937,10 +1976,17 @@ int pvq_alloc(Pvq* P, uint32_t len, bool reserved, uint64_t* id) {
 // digest and tag, and publish when the group is full or the device idle.
 int pvq_enqueue(Pvq* P, uint64_t id, uint32_t len, const uint8_t expected[20], uint64_t tag) {
     int rc;
-    // a group never wraps the slot ring: close it where the ring wraps
-    if (P->slot_tail != 0 && (P->slot_tail % P->nslots) == 0 && (rc = pvq_publish(P))) return rc;
-    if ((rc = pvq_wait(P, [&] { return P->slot_tail + 1 - P->slot_head <= P->nslots; }, "slot ring full")))
-        return rc;
+    // A group never wraps the slot ring: an open group that ends where the
+    // ring wraps is closed first.  pvq_wait sleeps without the queue's lock,
+    // so another thread may fill the ring's last slot meanwhile and leave its
+    // group open there: check again after every wait, under the
+    // lock, until the next slot does not continue a group across the wrap.
+    for (;;) {
+        if (P->open_count && P->slot_tail % P->nslots == 0 && (rc = pvq_publish(P))) return rc;
+        if ((rc = pvq_wait(P, [&] { return P->slot_tail + 1 - P->slot_head <= P->nslots; }, "slot ring full")))
+            return rc;
+        if (!(P->open_count && P->slot_tail % P->nslots == 0)) break;
+    }
     PvqRegion& r = P->regions[id - P->reg_base];
     const uint64_t sl = P->slot_tail % P->nslots;
     P->off[sl] = r.start % P->nbytes;
@@ -2153,7 +2199,7 @@ void* s1be_vq_create(size_t batch, uint32_t max_chunk_len) {
     const size_t hbytes = q->meta + q->cap * q->stride;
     for (auto& S : q->set) {
         if (S.h.ensure(hbytes) || S.d.ensure(hbytes + q->cap * 21) || S.res.ensure(q->cap) ||
-            hipStreamCreateWithFlags(&S.stream, hipStreamNonBlocking) != hipSuccess ||
+            vq_stream_create(&S.stream) != 0 ||
             hipEventCreateWithFlags(&S.done, hipEventDisableTiming) != hipSuccess) {
             if (t_err.empty()) fail(SHA1CHUNK_ENOMEM, "vq: allocation failed");
             s1be_vq_destroy(q);

@@ -12,9 +12,12 @@ error behaviour; file:line into /root/reference):
     SHA1()  .init/.update/.final    sha.h:58-60      streaming context
 
 plus the batch / device entry points of include/sha1chunk.h that replace a
-loop of shahash() calls.  Every digest is computed by the gfx950 HIP kernels
-(unless the process opts into SHA1CHUNK_HOST_SMALL for small calls, which
-still needs the device); there is no CPU fallback.  The library must have been built (`make -C
+loop of shahash() calls.  The batch, device and verify-queue calls run on
+the gfx950 HIP kernels; the reference's single-message calls (shahash,
+get_chunk_hash, verify_hash, the SHA1 trio, make_chunks on a file of at most
+4 MiB) hash on the host by default, as SURVEY.md 7.1 step 2 asks, and on the
+kernels under SHA1CHUNK_HOST_SMALL=0 (include/sha1chunk.h, "Routing").  A
+gfx950 device is required either way: there is no CPU fallback.  The library must have been built (`make -C
 congestion-control-with-bittorren_amd` or __graft_entry__.build()); a missing
 library or device raises, it never falls back.
 
@@ -84,6 +87,7 @@ _SIGNATURES = [
     ("seek_to_chunk_pos", None, [_vp, C.c_size_t]),
     ("seek_to_packet_pos", None, [_vp, C.c_size_t, C.c_size_t]),
     ("sha1chunk_hash_batch", C.c_int, [_vp, _u64p, _u32p, C.c_size_t, _u8p, C.c_uint]),
+    ("sha1chunk_digest", C.c_int, [_vp, C.c_uint64, _u8p]),
     ("sha1chunk_verify_batch", C.c_int, [_vp, _u64p, _u32p, C.c_size_t, _u8p, _u8p, C.c_uint]),
     ("sha1chunk_hash_device_async", C.c_int, [_vp, _vp, _vp, C.c_size_t, _vp, _vp, C.c_int]),
     ("sha1chunk_hash_uniform_async", C.c_int, [_vp, C.c_uint32, C.c_size_t, _vp, _vp, C.c_int]),
@@ -187,17 +191,16 @@ def hex2binary(hexstr: str) -> bytes:
 
 
 def shahash(data: bytes | np.ndarray) -> bytes:
-    """chunk.c:35-51 -- SHA-1 of data on the device."""
+    """chunk.c:35-51 -- SHA-1 of one message (sha1chunk_digest: on the host
+    by default, on the kernels under SHA1CHUNK_HOST_SMALL=0; a device is
+    required either way).  Raises instead of exit(-1)."""
     buf = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else \
         np.ascontiguousarray(data, np.uint8).reshape(-1)
     n = buf.size
     if n == 0:
         buf = np.zeros(1, np.uint8)
     out = np.zeros(DIGEST_LEN, np.uint8)
-    off = np.zeros(1, np.uint64)
-    ln = np.array([n], np.uint32)
-    _check(lib().sha1chunk_hash_batch(buf.ctypes.data, _np_ptr(off, _u64p), _np_ptr(ln, _u32p), 1,
-                                      _np_ptr(out), HOST), "shahash")
+    _check(lib().sha1chunk_digest(buf.ctypes.data, n, _np_ptr(out)), "shahash")
     return out.tobytes()
 
 

@@ -18,14 +18,22 @@
  * Error convention: 0 on success, a negative SHA1CHUNK_E* code otherwise
  * (never exit()); sha1chunk_last_error() returns a thread-local message.
  * There is no CPU fallback: without a usable gfx950 device every call
- * fails with SHA1CHUNK_ENODEV.  Opt-in (off by default): with
- * SHA1CHUNK_HOST_SMALL=<bytes> in the environment, host calls of at most
- * that many bytes (sha1chunk_hash_batch / verify_batch on host memory,
- * compress_blocks, finish: shahash, get_chunk_hash, verify_hash, the
- * SHA1Update trio; sha1chunk_hash_fd / make_chunks on a regular file of at
- * most that size; a verify queue of batch 1 whose max length fits) are hashed
- * on the host (x86 SHA extensions) -- one 512 KiB chunk in ~0.2 ms instead
- * of one lane's ~6 ms serial chain -- and the device is still required.
+ * fails with SHA1CHUNK_ENODEV, the host-routed calls below included.
+ *
+ * Routing.  One message is one serial chain of
+ * compressions: a GPU lane runs it at ~85 MB/s, a CPU core with the x86 SHA
+ * extensions at ~2.5 GB/s.  So by default the reference's single-message
+ * calls hash on the host: sha1chunk_compress_blocks / sha1chunk_finish (the
+ * SHA1Update / SHA1Final trio), shahash and what is built on it
+ * (get_chunk_hash, verify_hash, verify_chunk_hash's per-call path), and
+ * sha1chunk_hash_fd (make_chunks) on a regular file of at most 4 MiB --
+ * one 512 KiB chunk in ~0.2 ms instead of one lane's ~6 ms.  Every batch,
+ * device and verify-queue entry point, and make_chunks on larger files and
+ * streams, runs on the gfx950 kernels.  SHA1CHUNK_HOST_SMALL in the
+ * environment (read once per process) changes this: "0" puts every call on
+ * the kernels; "<bytes>" hashes every host call of at most that many bytes
+ * on the host (batches, the trio, a regular file, a verify queue of batch 1
+ * whose max length fits) and larger ones on the kernels.
  */
 #ifndef SHA1CHUNK_H
 #define SHA1CHUNK_H
@@ -73,6 +81,12 @@ enum {
  * Synchronous.  Host mode accepts any alignment and overlapping chunks. */
 int sha1chunk_hash_batch(const void *base, const uint64_t *offsets, const uint32_t *lengths,
                          size_t n, uint8_t *digests, unsigned flags);
+
+/* One message's digest, routed as the reference's single-message calls are
+ * (shahash, chunk.c:35-51, is this call): on the host by default, on the
+ * kernels under SHA1CHUNK_HOST_SMALL=0 or above an explicit threshold
+ * (routing above).  len <= 2^32 - 1 on the kernels. */
+int sha1chunk_digest(const void *msg, uint64_t len, uint8_t digest[20]);
 
 /* mismatch[i] = 0 if the digest of chunk i equals expected[i*20..], else 1
  * (the verify_hash() convention of job.c:217-228). */
@@ -176,7 +190,7 @@ int sha1chunk_synth_fill_ragged_async(void *d_base, const uint64_t *d_offsets,
  * therefore always come back through poll() without a flush.  Three batch
  * sets are in flight at once.
  *
- * batch == 1 with SHA1CHUNK_HOST_SMALL >= max_chunk_len (opt-in): the
+ * batch == 1 with SHA1CHUNK_HOST_SMALL >= max_chunk_len (explicit opt-in): the
  * batch-size-1 host path.  Each submit hashes and compares its chunk on the
  * host before returning (0.2 ms per 512 KiB instead of a 6 ms device chain);
  * poll() returns the results in submission order.  A device is still
@@ -209,8 +223,11 @@ int sha1chunk_vq_submit(sha1chunk_vq *q, const void *chunk, uint32_t len,
  * result is polled, until release() (after the caller copied the verified
  * chunk into its job buffer, reliable_udp.c:696-709, or dropped it).  A
  * reservation may also be released without a commit.  Unreleased buffers
- * hold ring space: reserve() fails (NULL, SHA1CHUNK_ENOMEM) rather than
- * wait when only the caller can free the room it needs.  In batch mode and
+ * hold ring space.  reserve() and submit() wait (bounded) for room while
+ * in-flight chunks or other threads' reservations hold it; they fail (NULL,
+ * resp. SHA1CHUNK_ENOMEM) rather than wait when the ring's oldest region is
+ * the calling thread's own reservation, not committed or not released --
+ * room only that thread could free.  In batch mode and
  * on the batch-1 host path the buffer is ordinary host memory (commit
  * copies it, resp. hashes it in place). */
 void *sha1chunk_vq_reserve(sha1chunk_vq *q, uint32_t len);

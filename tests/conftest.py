@@ -10,6 +10,24 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 GOLDEN_DIR = os.path.join(ROOT, "tests", "golden")
 
+# Pin every call of this test process (and of the child processes it starts,
+# unless a test sets its own value) to the gfx950 kernels.  By default the
+# library hashes the reference's single-message calls (shahash, verify_hash,
+# the SHA1Update trio, make_chunks on a file <= 4 MiB) on the host
+# (csrc/frontend.c routing); the kernel-parity tests must reach the kernels
+# with those calls too.  The default routing has its own tests
+# (test_host_small.py::test_default_routing_gpu, test_config1_make_chunks_cli),
+# which start their children without this variable (default_env()).
+os.environ["SHA1CHUNK_HOST_SMALL"] = "0"
+
+
+def default_env(**extra) -> dict:
+    """This process's environment without the test pin: the library's
+    default routing, plus `extra`."""
+    env = {k: v for k, v in os.environ.items() if k != "SHA1CHUNK_HOST_SMALL"}
+    env.update(extra)
+    return env
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) device")

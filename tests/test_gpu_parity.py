@@ -9,6 +9,8 @@ import time
 import numpy as np
 import pytest
 
+from conftest import default_env
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 PKG_DIR = os.path.join(ROOT, "congestion-control-with-bittorren_amd")
@@ -273,23 +275,27 @@ def test_config1_make_chunks_cli(pkg, dev, golden, fixture_files, tmp_path):
     """BASELINE config 1 (make-chunks on tmp/C.tar, 4 chunks), every way the
     CLI can run here, each against tmp/C.chunks: the reference's own
     make-chunks built from its sources (oracle/_ref, CPU sha.c), the repo's
-    CLI (device, and the host small-file path with SHA1CHUNK_HOST_SMALL at
-    4 MiB), and the reference main linked against the library with the knob.
+    CLI (the default routing, which hashes this 2 MiB file on the host; the
+    kernels, SHA1CHUNK_HOST_SMALL=0; the explicit 4 MiB knob), and the
+    reference main linked against the library (default and kernels).
     Prints the median wall time of 5 runs of each (process start included)."""
     p = tmp_path / "C.tar"
     p.write_bytes(fixture_files["tmp/C.tar"])
     want = "".join(f"{i} {h}\n" for i, h in enumerate(golden["fixtures"]["C.chunks_file"]))
-    runs = {"repo_cli_device": (os.path.join(PKG_DIR, "make-chunks"), {}),
-            "repo_cli_host_small": (os.path.join(PKG_DIR, "make-chunks"), {"SHA1CHUNK_HOST_SMALL": "4194304"})}
+    cli = os.path.join(PKG_DIR, "make-chunks")
+    runs = {"repo_cli_default": (cli, None),  # the library's default routing: host for a <= 4 MiB file
+            "repo_cli_device": (cli, {"SHA1CHUNK_HOST_SMALL": "0"}),
+            "repo_cli_host_small": (cli, {"SHA1CHUNK_HOST_SMALL": "4194304"})}
     ref_exe = os.path.join(ROOT, "oracle", "_ref", "make-chunks")
     dropin = os.path.join(ROOT, "oracle", "_ref", "dropin", "make-chunks")
     if os.path.exists(ref_exe):
         runs["reference_sha_c"] = (ref_exe, {})
     if os.path.exists(dropin):
-        runs["reference_main_dropin_host_small"] = (dropin, {"SHA1CHUNK_HOST_SMALL": "4194304"})
+        runs["reference_main_dropin_default"] = (dropin, None)
+        runs["reference_main_dropin_device"] = (dropin, {"SHA1CHUNK_HOST_SMALL": "0"})
     times = {}
     for name, (exe, extra) in runs.items():
-        env = dict(os.environ, **extra)
+        env = default_env() if extra is None else dict(os.environ, **extra)
         ts = []
         for _ in range(5):
             t0 = time.perf_counter()

@@ -128,6 +128,69 @@ def test_rings_wrap_many_times(pkg, dev, persistent, monkeypatch, oracle):
     assert got == want
 
 
+def test_slot_ring_wraps_under_many_threads(pkg, dev, persistent, monkeypatch):
+    """eight threads share one queue of tiny chunks, half
+    through submit, half through reserve -> commit -> release, with a 1 MiB
+    data ring (1024 slots, so the slot ring, not the data ring, fills) and an
+    8-CU drain (groups stay open up to 64 chunks while 8 are in flight): the
+    slot ring wraps ~20 times while threads sleep in the full-ring wait and
+    others fill the ring's last slot.  A group must never span the wrap (the
+    drain indexes a group's slots without a modulo); every result is right
+    (10 % wrong expected digests) and comes back exactly once."""
+    import threading
+    monkeypatch.setenv("SHA1CHUNK_VQ_RING_MIB", "1")
+    monkeypatch.setenv("SHA1CHUNK_VQ_CUS", "8")
+    rng = np.random.default_rng(55)
+    data = rng.integers(0, 256, 8192, dtype=np.uint8).tobytes()
+    per, nthreads = 2500, 8
+    want, got, errors = {}, {}, []
+    lock = threading.Lock()
+
+    def collect(res):
+        with lock:
+            for tag, m in res:
+                assert tag not in got, tag
+                got[tag] = m
+
+    with pkg.VerifyQueue(batch=64, max_chunk_len=4096) as q:
+        def worker(k):
+            try:
+                r = np.random.default_rng(1000 + k)
+                for i in range(per):
+                    tag = k * 100000 + i
+                    L = int(r.integers(0, 257))
+                    s0 = int(r.integers(0, 4096))
+                    b = data[s0:s0 + L]
+                    d = hashlib.sha1(b).digest()
+                    bad = i % 10 == 3
+                    if bad:
+                        d = bytes([d[0] ^ 0x80]) + d[1:]
+                    with lock:
+                        want[tag] = int(bad)
+                    if k % 2:
+                        q.submit(b, d, tag)
+                    else:
+                        rv = q.reserve(L)
+                        rv.view[:] = np.frombuffer(b, np.uint8)
+                        q.commit(rv, d, tag)
+                        q.release(rv)  # freed once its result is collected
+                    if i % 97 == 0:
+                        collect(q.poll())
+            except Exception as e:  # surfaced below
+                errors.append(repr(e))
+
+        ts = [threading.Thread(target=worker, args=(k,)) for k in range(nthreads)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join(timeout=120)
+        assert not errors, errors[:3]
+        assert not any(t.is_alive() for t in ts)
+        collect(q.poll(wait=True, max_results=1 << 16))
+        assert q.pending == 0
+    assert got == want
+
+
 def test_throughput_512k_chunks(pkg, dev, persistent):
     """4096 x 512 KiB host chunks (2 GiB) through the persistent queue with
     batch 64: every result right; the rate (PCIe-bound: the drain reads the

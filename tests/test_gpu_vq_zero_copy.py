@@ -156,6 +156,58 @@ def test_full_ring_of_unreleased_buffers_fails_fast(pkg, dev, monkeypatch):
             q.release(h)
 
 
+def test_another_threads_reservation_makes_submit_wait(pkg, dev, monkeypatch):
+    """on a queue shared by receive threads, another
+    session's reservation at the ring's head is a buffer still filling, not a
+    dead end: this thread's submits and reserves wait for it (bounded) instead
+    of failing with ENOMEM.  A session thread reserves the ring's first
+    buffer, fills it 0.3 s later, commits and releases it; meanwhile the main
+    thread submits three rings' worth of chunks.  Every submit succeeds, none
+    before the session's commit could free the head, every result is right."""
+    import threading
+    monkeypatch.setenv("SHA1CHUNK_VQ_MODE", "persistent")
+    monkeypatch.setenv("SHA1CHUNK_VQ_RING_MIB", "8")  # 128 chunks of 64 KiB
+    chunk = bytes(range(256)) * 256
+    dig = hashlib.sha1(chunk).digest()
+    with pkg.VerifyQueue(batch=64, max_chunk_len=65536) as q:
+        reserved, committed = threading.Event(), threading.Event()
+        errors = []
+
+        def session():  # the session's own thread reserves, fills, commits, releases
+            try:
+                r0 = q.reserve(65536)
+                reserved.set()
+                time.sleep(0.3)
+                r0.view[:] = np.frombuffer(chunk, np.uint8)
+                committed.set()
+                q.commit(r0, dig, 10**6)
+                q.release(r0)
+            except Exception as e:
+                errors.append(repr(e))
+                reserved.set()
+
+        t = threading.Thread(target=session)
+        t.start()
+        try:
+            assert reserved.wait(timeout=30) and not errors, errors
+            t0 = time.time()
+            got = {}
+            for i in range(3 * 128):
+                q.submit(chunk, dig if i % 7 else bytes(20), i)
+                if i == 127:  # the ring's 128th buffer: room only once the session's head buffer is freed
+                    assert committed.is_set() and time.time() - t0 >= 0.25
+                for tag, m in q.poll():
+                    got[tag] = m
+        finally:
+            t.join(timeout=60)  # destroy must not overlap the session's calls
+        assert not errors and committed.is_set(), errors
+        for tag, m in q.poll(wait=True, max_results=1 << 16):
+            got[tag] = m
+        want = {i: (0 if i % 7 else 1) for i in range(3 * 128)}
+        want[10**6] = 0
+        assert got == want
+
+
 def test_queue_create_destroy_beside_a_busy_queue(pkg, dev, corpus, monkeypatch):
     """creating and destroying a queue must not wait for the
     whole device.  One thread keeps a persistent queue continuously busy for
@@ -256,3 +308,86 @@ def test_five_busy_queues_and_a_device_batch(pkg, dev, corpus, monkeypatch):
             t.join(timeout=120)
     assert not errors, errors
     assert all(c > 0 for c in counts), counts
+
+
+def _config2_on_fresh_stream(pkg, dev):
+    """One config-2 batch (4096 x 512 KiB, device-resident) hashed on a new
+    stream: wall seconds from the launch to the stream's completion, and
+    whether its digests equal the reference's golden ones."""
+    n = 4096
+    buf = dev.empty(n * L512, dtype=dev.uint8, device="cuda")
+    dig = dev.zeros((n, 20), dtype=dev.uint8, device="cuda")
+    st = dev.cuda.Stream()
+    st.wait_stream(dev.cuda.current_stream())
+    pkg.synth_fill_device(buf, 0, n, L512, stream=st)
+    st.synchronize()
+    t0 = time.perf_counter()
+    pkg.hash_uniform_device(buf, L512, n, dig, stream=st)
+    st.synchronize()
+    secs = time.perf_counter() - t0
+    gold = np.fromfile(os.path.join(ROOT, "tests/golden/synth_4096x512k.bin"), np.uint8).reshape(-1, 20)
+    ok = np.array_equal(dig.cpu().numpy(), gold)
+    del buf, dig
+    return secs, ok
+
+
+def test_wait_behind_busy_drains_is_bounded(pkg, dev, corpus, monkeypatch):
+    """a config-2 batch launched on a fresh stream while
+    four verify queues are continuously fed finishes within its solo time +
+    10 ms (the bound stated in include/sha1chunk.h): no drain holds a
+    hardware queue the batch's stream is mapped to for longer than that."""
+    import threading
+    monkeypatch.setenv("SHA1CHUNK_VQ_MODE", "persistent")
+    monkeypatch.setenv("SHA1CHUNK_VQ_RING_MIB", "256")
+    import sys
+    host, want = corpus
+    # the feeders' bytes made once: their loop then holds the GIL for a few
+    # microseconds per submit (the C call releases it), so the timed thread's
+    # wall clock measures the device, not the interpreter
+    chunks = [host[i].tobytes() for i in range(64)]
+    digs = [want[i].tobytes() for i in range(64)]
+    old_switch = sys.getswitchinterval()
+    sys.setswitchinterval(1e-4)
+    solo = min(_config2_on_fresh_stream(pkg, dev)[0] for _ in range(3))
+    stop, started = threading.Event(), threading.Barrier(5)
+    errors, counts = [], [0] * 4
+
+    def feeder(k):
+        try:
+            with pkg.VerifyQueue(batch=64, max_chunk_len=L512) as q:
+                started.wait(timeout=60)
+                i = 0
+                while not stop.is_set():
+                    q.submit(chunks[i % 64], digs[i % 64], i)
+                    i += 1
+                    if i % 32 == 0:
+                        res = q.poll()
+                        assert all(m == 0 for _, m in res)
+                        counts[k] += len(res)
+                res = q.poll(wait=True)
+                assert all(m == 0 for _, m in res)
+                counts[k] += len(res)
+        except Exception as e:
+            errors.append(e)
+
+    ts = [threading.Thread(target=feeder, args=(k,)) for k in range(4)]
+    for t in ts:
+        t.start()
+    busy = []
+    try:
+        started.wait(timeout=60)
+        time.sleep(0.5)
+        for _ in range(5):
+            secs, ok = _config2_on_fresh_stream(pkg, dev)
+            assert ok
+            busy.append(secs)
+    finally:
+        stop.set()
+        for t in ts:
+            t.join(timeout=120)
+        sys.setswitchinterval(old_switch)
+    assert not errors, errors
+    assert all(c > 0 for c in counts), counts
+    print(f"config-2 batch on a fresh stream: solo {solo * 1e3:.2f} ms, beside 4 fed queues "
+          f"{', '.join(f'{b * 1e3:.2f}' for b in busy)} ms")
+    assert max(busy) <= solo + 0.010, (solo, busy)
