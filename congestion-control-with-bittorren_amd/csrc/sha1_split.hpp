@@ -132,6 +132,15 @@ __device__ __forceinline__ void split_barrier() {
     asm volatile("s_barrier" ::: "memory");
 }
 
+// Study probe (A/B library only, kVProbe): the same barrier, with the
+// shader-clock cycles the wave spends in it added to `acc`.
+__device__ __forceinline__ void split_barrier_timed(uint64_t& acc) {
+    __builtin_amdgcn_s_waitcnt(0xC07F);
+    const uint64_t t0 = __builtin_amdgcn_s_memtime();
+    asm volatile("s_barrier" ::: "memory");
+    acc += __builtin_amdgcn_s_memtime() - t0;
+}
+
 // Producer: the 80-word schedule of one block, plus K, into its W block slot.
 template <int T, bool WK>
 struct SchedWrite {
@@ -192,11 +201,17 @@ __device__ __forceinline__ void tail_block_words(const Entry& en, uint32_t k, ui
 // one block per unit and ends the unit after it.  A single producer ends the
 // unit after block U-1.
 template <int U, bool WK, int NPROD = 1>
-__device__ __forceinline__ void produce_block(uint32_t k, uint32_t (&w)[16], uint8_t* ring, int lane) {
+__device__ __forceinline__ void produce_block(uint32_t k, uint32_t (&w)[16], uint8_t* ring, int lane,
+                                              uint64_t* bw = nullptr) {
     const uint32_t m = k / U, j = k - m * U;
     SchedWrite<0, WK>::run(w, ring + ((m & 1u) * U + j) * kWBlockBytes, lane);
     // U == NPROD: each producer writes one block of every unit
-    if (NPROD == 1 ? j == U - 1 : (U == NPROD || (k & 1u) == 1u)) split_barrier();
+    if (NPROD == 1 ? j == U - 1 : (U == NPROD || (k & 1u) == 1u)) {
+        if (bw)
+            split_barrier_timed(*bw);
+        else
+            split_barrier();
+    }
 }
 
 
@@ -240,7 +255,11 @@ __device__ __forceinline__ void load_stage(const uint8_t* p, Stage& st) {
 // reads (each of ds_read_b128's 16-lane groups sees 16 distinct 16-byte
 // bank groups).
 constexpr uint32_t kCoopStageBytes = 64u * 128u;
-constexpr uint32_t kCoopWaveBytes = 2u * kCoopStageBytes;
+// A fused wave's LDS in the mixed kernel: five 4 KiB block buffers of the
+// LDS-DMA loop below (eight fused waves fill the workgroup's 160 KiB).
+constexpr uint32_t kCoopBlockBytes = 64u * 64u;
+constexpr uint32_t kCoopBlockBufs = 5u;
+constexpr uint32_t kCoopWaveBytes = kCoopBlockBufs * kCoopBlockBytes;
 
 // Orders one wave's LDS accesses across a transpose: lane-to-lane exchange
 // through LDS (coop_store -> coop_read, and the reads of a buffer before its
@@ -381,7 +400,8 @@ __device__ __forceinline__ void produce_stage_coop(const u32x4u* const (&src)[8]
 
 template <int U, bool WK, int NPROD>
 __device__ __forceinline__ void produce_own_block_coop(const u32x4u* const (&src)[4], uint32_t k, uint32_t K,
-                                                       uint32_t (&cur)[16], uint8_t* ring, uint32_t lane) {
+                                                       uint32_t (&cur)[16], uint8_t* ring, uint32_t lane,
+                                                       uint64_t* bw = nullptr) {
     const uint32_t m = k / U, j = k - m * U;
     uint8_t* raw = ring + ((m & 1u) * U + j) * kWBlockBytes;
     coop4_store(raw, cur, lane);
@@ -392,19 +412,20 @@ __device__ __forceinline__ void produce_own_block_coop(const u32x4u* const (&src
     wave_lds_order();  // the W writes below overwrite what was just read
 #pragma unroll
     for (int q = 0; q < 16; ++q) w[q] = bswap(w[q]);
-    produce_block<U, WK, NPROD>(k, w, ring, (int)lane);
+    produce_block<U, WK, NPROD>(k, w, ring, (int)lane, bw);
 }
 
 // Producer that owns one block per unit (U == NPROD): block k from `cur`,
 // which is then refilled with this producer's block after next, k + 2 NPROD.
 template <int U, bool WK, int NPROD>
 __device__ __forceinline__ void produce_own_block(const Entry& en, uint32_t k, uint32_t K,
-                                                  uint32_t (&cur)[16], uint8_t* ring, int lane) {
+                                                  uint32_t (&cur)[16], uint8_t* ring, int lane,
+                                                  uint64_t* bw = nullptr) {
     uint32_t w[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) w[j] = bswap(cur[j]);
     if (k + 2 * NPROD < K) load_block16(en.p + 64ull * (k + 2 * NPROD), cur);
-    produce_block<U, WK, NPROD>(k, w, ring, lane);
+    produce_block<U, WK, NPROD>(k, w, ring, lane, bw);
 }
 
 template <int P>
@@ -474,10 +495,34 @@ constexpr int kSplitV = U == 4 ? (kVWK | kVUnmask | kVSkipWave2 | kVRead10 | kVC
 template <int U>
 constexpr int kSplitNProd = U == 4 ? 2 : 1;
 
-template <int U, int J, int V, bool MASK>
+// Round-5 study flag (the 8-wave two-pair shape): the second pair's
+// consumer issues its schedule-read bursts half a burst interval later than
+// the first's.  Both pairs pass the workgroup's shared s_barrier together,
+// so without it their read bursts (each 5 or 10 ds_read_b128 of 1 KiB) hit
+// the CU's one LDS pipe at the same moments.
+constexpr int kVPhase = 512;
+// Round-5 study flag: the consumer times its barrier waits and its whole
+// loop (shader clock) and writes them over its group's first digest rows
+// instead of digests (wrong digests by design; A/B library only).
+constexpr int kVProbe = 2048;
+// Round-5 study flag: the pairs' read bursts both off the barrier, at
+// rounds 10 / 50 (first pair) and 30 / 70 (second pair), with kVRead10.
+constexpr int kVPhase2 = 4096;
+template <int V>
+__device__ __forceinline__ void split_barrier_or_timed(uint64_t& acc) {
+    if constexpr ((V & kVProbe) != 0)
+        split_barrier_timed(acc);
+    else
+        split_barrier();
+}
+// Round-5 study flag: all 20 schedule reads of the next block in one burst
+// (before round 0, or before round 40 for the second pair under kVPhase).
+constexpr int kVRead20 = 1024;
+
+template <int U, int J, int V, bool MASK, int PH = 0>
 __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (&h)[5],
                                               const uint32_t (&Wc)[80], uint32_t (&Wn)[80],
-                                              const uint8_t* ring, int lane) {
+                                              const uint8_t* ring, int lane, uint64_t& bw) {
     // Block k+1 (k = k0 + J, k0 a multiple of 2U) is unit (k0/U + (J+1)/U),
     // whose parity is that of (J+1)/U since k0/U is even, and sub-block
     // (J+1) % U: the slot address is a compile-time offset.  A barrier goes
@@ -487,35 +532,53 @@ __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (
     constexpr int slot_idx = (((J + 1) / U) & 1) * U + jn;
     const uint8_t* slot = ring + slot_idx * kWBlockBytes + lane * 16;
     uint32_t v[5] = {h[0], h[1], h[2], h[3], h[4]};
-    if constexpr ((V & kVRead10) != 0) {
-        if constexpr (jn == 0) split_barrier();
-        // two bursts of 10 reads (before rounds 0 and 40)
+    if constexpr ((V & kVRead20) != 0) {
+        constexpr int R = PH != 0 ? 40 : 0;
+        if constexpr (jn == 0) split_barrier_or_timed<V>(bw);
+        RoundsW<0, R, WK>::run(v, Wc);
+        __builtin_amdgcn_sched_barrier(0);
+        read_w_group<0>(slot, Wn);
+        read_w_group<1>(slot, Wn);
+        read_w_group<2>(slot, Wn);
+        read_w_group<3>(slot, Wn);
+        __builtin_amdgcn_sched_barrier(0);
+        RoundsW<R, 80, WK>::run(v, Wc);
+    } else if constexpr ((V & kVRead10) != 0) {
+        // two bursts of 10 reads, before rounds 10 PH and 10 PH + 40
+        constexpr int R = 10 * PH;
+        if constexpr (jn == 0) split_barrier_or_timed<V>(bw);
+        RoundsW<0, R, WK>::run(v, Wc);
+        __builtin_amdgcn_sched_barrier(0);
         read_w_group<0>(slot, Wn);
         read_w_group<1>(slot, Wn);
         __builtin_amdgcn_sched_barrier(0);
-        RoundsW<0, 40, WK>::run(v, Wc);
+        RoundsW<R, R + 40, WK>::run(v, Wc);
         __builtin_amdgcn_sched_barrier(0);
         read_w_group<2>(slot, Wn);
         read_w_group<3>(slot, Wn);
         __builtin_amdgcn_sched_barrier(0);
-        RoundsW<40, 80, WK>::run(v, Wc);
+        RoundsW<R + 40, 80, WK>::run(v, Wc);
     } else {
-        if constexpr (jn == 0) split_barrier();
+        // four bursts of 5 reads, before rounds R, R + 20, R + 40, R + 60
+        constexpr int R = PH != 0 ? 10 : 0;
+        if constexpr (jn == 0) split_barrier_or_timed<V>(bw);
+        RoundsW<0, R, WK>::run(v, Wc);
+        __builtin_amdgcn_sched_barrier(0);
         read_w_group<0>(slot, Wn);
         __builtin_amdgcn_sched_barrier(0);
-        RoundsW<0, 20, WK>::run(v, Wc);
+        RoundsW<R, R + 20, WK>::run(v, Wc);
         __builtin_amdgcn_sched_barrier(0);
         read_w_group<1>(slot, Wn);
         __builtin_amdgcn_sched_barrier(0);
-        RoundsW<20, 40, WK>::run(v, Wc);
+        RoundsW<R + 20, R + 40, WK>::run(v, Wc);
         __builtin_amdgcn_sched_barrier(0);
         read_w_group<2>(slot, Wn);
         __builtin_amdgcn_sched_barrier(0);
-        RoundsW<40, 60, WK>::run(v, Wc);
+        RoundsW<R + 40, R + 60, WK>::run(v, Wc);
         __builtin_amdgcn_sched_barrier(0);
         read_w_group<3>(slot, Wn);
         __builtin_amdgcn_sched_barrier(0);
-        RoundsW<60, 80, WK>::run(v, Wc);
+        RoundsW<R + 60, 80, WK>::run(v, Wc);
     }
     if constexpr (MASK) {
         const bool live = k < T;
@@ -529,17 +592,58 @@ __device__ __forceinline__ void consume_block(uint32_t k, uint32_t T, uint32_t (
 
 // 2U blocks (two units) per consumer iteration, unrolled, so Wa/Wb keep
 // their parity and every barrier position is a compile-time constant.
-template <int U, int J, int V, bool MASK>
+template <int U, int J, int V, bool MASK, int PH = 0>
 struct ConsumeUnits {
     __device__ __forceinline__ static void run(uint32_t k0, uint32_t T, uint32_t (&h)[5],
                                                uint32_t (&Wa)[80], uint32_t (&Wb)[80],
-                                               const uint8_t* ring, int lane) {
+                                               const uint8_t* ring, int lane, uint64_t& bw) {
         if constexpr (J < 2 * U) {
-            consume_block<U, J, V, MASK>(k0 + J, T, h, Wa, Wb, ring, lane);
-            ConsumeUnits<U, J + 1, V, MASK>::run(k0, T, h, Wb, Wa, ring, lane);
+            consume_block<U, J, V, MASK, PH>(k0 + J, T, h, Wa, Wb, ring, lane, bw);
+            ConsumeUnits<U, J + 1, V, MASK, PH>::run(k0, T, h, Wb, Wa, ring, lane, bw);
         }
     }
 };
+
+// The consumer wave of a split pair: every block's 80 rounds, W+K from the
+// ring (see split_body).
+template <int U, int V, int PH>
+__device__ __forceinline__ void consume_all(const BatchArgs& A, const Entry& en, bool valid, uint32_t T,
+                                            uint32_t units, const uint8_t* ring, int lane) {
+    uint32_t h[5];
+    load_init(A, en.id, h);
+    uint32_t Wa[80], Wb[80];
+    split_barrier();  // B_0
+    read_w_group<0>(ring + lane * 16, Wa);
+    read_w_group<1>(ring + lane * 16, Wa);
+    read_w_group<2>(ring + lane * 16, Wa);
+    read_w_group<3>(ring + lane * 16, Wa);
+    // Iterations in which every valid lane is still inside its chunk
+    // commit without the per-lane select (all of them for equal lengths).
+    const uint32_t Tmin = __builtin_amdgcn_readfirstlane(wave_min(valid ? T : 0xffffffffu));
+    const uint32_t full = (V & kVUnmask) ? min(Tmin, units * U) / (2 * U) * (2 * U) : 0u;
+    uint32_t k = 0;
+    uint64_t bw = 0;
+    const uint64_t t0 = (V & kVProbe) ? __builtin_amdgcn_s_memtime() : 0;
+    for (; k < full; k += 2 * U) {
+        ConsumeUnits<U, 0, V, false, PH>::run(k, T, h, Wa, Wb, ring, lane, bw);
+    }
+    for (; k < units * U; k += 2 * U) {
+        ConsumeUnits<U, 0, V, true, PH>::run(k, T, h, Wa, Wb, ring, lane, bw);
+    }
+    if constexpr ((V & kVProbe) != 0) {
+        const uint64_t tot = __builtin_amdgcn_s_memtime() - t0;
+        if (lane == 0) {  // over the group's first digest row
+            uint32_t* o = reinterpret_cast<uint32_t*>(A.dig + 20ull * (en.id & ~63u));
+            o[0] = (uint32_t)bw;
+            o[1] = (uint32_t)(bw >> 32);
+            o[2] = (uint32_t)tot;
+            o[3] = (uint32_t)(tot >> 32);
+            o[4] = units * U;
+        }
+        return;
+    }
+    if (valid) emit(A, en.id, h);
+}
 
 // PAIRS consumer/producer pairs per workgroup: waves 0..PAIRS-1 consume,
 // waves PAIRS..2*PAIRS-1 produce, pair p = (wave p, wave p+PAIRS).  Waves of
@@ -621,35 +725,49 @@ __device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uin
             const uint32_t K = S * 2u;
             uint32_t B0[16], B1[16];
             uint32_t k = pidx;
+            uint64_t pbw = 0;
+            uint64_t* const pb = (V & kVProbe) ? &pbw : nullptr;
+            const uint64_t pt0 = (V & kVProbe) ? __builtin_amdgcn_s_memtime() : 0;
             if constexpr ((V & kVCoop) != 0) {
                 const u32x4u* src[4];
                 coop_sources<4>(A, group, (uint32_t)lane, src);
                 if (pidx < K) coop4_load(src, pidx, B0);
                 if (pidx + NPROD < K) coop4_load(src, pidx + NPROD, B1);
                 for (; k + NPROD < K; k += 2 * NPROD) {
-                    produce_own_block_coop<U, WK, NPROD>(src, k, K, B0, ring, (uint32_t)lane);
-                    produce_own_block_coop<U, WK, NPROD>(src, k + NPROD, K, B1, ring, (uint32_t)lane);
+                    produce_own_block_coop<U, WK, NPROD>(src, k, K, B0, ring, (uint32_t)lane, pb);
+                    produce_own_block_coop<U, WK, NPROD>(src, k + NPROD, K, B1, ring, (uint32_t)lane, pb);
                 }
                 if (k < K) {
-                    produce_own_block_coop<U, WK, NPROD>(src, k, K, B0, ring, (uint32_t)lane);
+                    produce_own_block_coop<U, WK, NPROD>(src, k, K, B0, ring, (uint32_t)lane, pb);
                     k += NPROD;
                 }
             } else {
                 if (pidx < K) load_block16(en.p + 64ull * pidx, B0);
                 if (pidx + NPROD < K) load_block16(en.p + 64ull * (pidx + NPROD), B1);
                 for (; k + NPROD < K; k += 2 * NPROD) {
-                    produce_own_block<U, WK, NPROD>(en, k, K, B0, ring, lane);
-                    produce_own_block<U, WK, NPROD>(en, k + NPROD, K, B1, ring, lane);
+                    produce_own_block<U, WK, NPROD>(en, k, K, B0, ring, lane, pb);
+                    produce_own_block<U, WK, NPROD>(en, k + NPROD, K, B1, ring, lane, pb);
                 }
                 if (k < K) {
-                    produce_own_block<U, WK, NPROD>(en, k, K, B0, ring, lane);
+                    produce_own_block<U, WK, NPROD>(en, k, K, B0, ring, lane, pb);
                     k += NPROD;
                 }
             }
             for (; k < units * U; k += NPROD) {
                 uint32_t w[16];
                 if (k < T) tail_block_words(en, k, w);
-                produce_block<U, WK, NPROD>(k, w, ring, lane);
+                produce_block<U, WK, NPROD>(k, w, ring, lane, pb);
+            }
+            if constexpr ((V & kVProbe) != 0) {
+                const uint64_t tot = __builtin_amdgcn_s_memtime() - pt0;
+                if (lane == 0) {  // over the group's digest row 1 + pidx
+                    uint32_t* o = reinterpret_cast<uint32_t*>(A.dig + 20ull * (group * 64u + 1u + pidx));
+                    o[0] = (uint32_t)pbw;
+                    o[1] = (uint32_t)(pbw >> 32);
+                    o[2] = (uint32_t)tot;
+                    o[3] = (uint32_t)(tot >> 32);
+                    o[4] = units * U;
+                }
             }
             split_barrier();  // matches the consumer's last (unused) read
             return;
@@ -697,26 +815,20 @@ __device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uin
         split_barrier();  // matches the consumer's last (unused) read
     } else {
         // ----------------------------- consumer -------------------------
-        uint32_t h[5];
-        load_init(A, en.id, h);
-        uint32_t Wa[80], Wb[80];
-        split_barrier();  // B_0
-        read_w_group<0>(ring + lane * 16, Wa);
-        read_w_group<1>(ring + lane * 16, Wa);
-        read_w_group<2>(ring + lane * 16, Wa);
-        read_w_group<3>(ring + lane * 16, Wa);
-        // Iterations in which every valid lane is still inside its chunk
-        // commit without the per-lane select (all of them for equal lengths).
-        const uint32_t Tmin = __builtin_amdgcn_readfirstlane(wave_min(valid ? T : 0xffffffffu));
-        const uint32_t full = (V & kVUnmask) ? min(Tmin, units * U) / (2 * U) * (2 * U) : 0u;
-        uint32_t k = 0;
-        for (; k < full; k += 2 * U) {
-            ConsumeUnits<U, 0, V, false>::run(k, T, h, Wa, Wb, ring, lane);
+        if constexpr ((V & kVPhase2) != 0) {
+            if (pair == 1)
+                consume_all<U, V, 3>(A, en, valid, T, units, ring, lane);
+            else
+                consume_all<U, V, 1>(A, en, valid, T, units, ring, lane);
+            return;
         }
-        for (; k < units * U; k += 2 * U) {
-            ConsumeUnits<U, 0, V, true>::run(k, T, h, Wa, Wb, ring, lane);
+        if constexpr ((V & kVPhase) != 0) {
+            if (pair == 1) {
+                consume_all<U, V, 2>(A, en, valid, T, units, ring, lane);
+                return;
+            }
         }
-        if (valid) emit(A, en.id, h);
+        consume_all<U, V, 0>(A, en, valid, T, units, ring, lane);
     }
 }
 
@@ -836,6 +948,35 @@ __device__ __forceinline__ void coop_compress(const uint32_t (&cur)[32], uint32_
     }
 }
 
+// LDS-DMA (global_load_lds_dwordx4): each lane's 16 bytes from its own
+// global address land at the wave-uniform LDS byte address `lds_dst` +
+// 16 x lane, with no VGPR and no ds_write.  M0 carries the LDS address and is
+// saved and restored in the same statement (hipcc reserves it).  hipcc does
+// not count these loads: the caller waits for them with an explicit
+// s_waitcnt vmcnt (and drains them before any load hipcc counts).
+typedef __attribute__((address_space(3))) uint8_t lds_u8;
+__device__ __forceinline__ uint32_t lds_addr(const uint8_t* p) {
+    return static_cast<uint32_t>(reinterpret_cast<uintptr_t>((const lds_u8*)p));
+}
+__device__ __forceinline__ void glds16(const void* src, uint32_t lds_dst) {
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(lds_dst)
+                 : "memory");
+}
+
+// Block k of the group's 64 chunks into the 4 KiB buffer at LDS address
+// `buf`: instruction i reads block k of chunks 16i .. 16i+15 (4 lanes per
+// chunk), lane l writing buf + i KiB + 16 l.  p[i] is lane l's source in
+// chunk 16i + l/4 at byte 16 x ((l%4 - l/16) & 3) of the block, so the LDS
+// image is coop4_store's swizzled one (piece q of chunk c at
+// c*64 + ((q + c/4) & 3)*16) and coop4_read hands each lane its chunk.
+__device__ __forceinline__ void glds_block(const uint8_t* const (&p)[4], uint32_t k, uint32_t buf) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) glds16(p[i] + 64ull * k, buf + 1024u * (uint32_t)i);
+}
+
 // lds: this wave's kCoopWaveBytes.  Same contract as fused_body.  The
 // wave's LDS accesses complete in order, so a stage's stores precede its
 // reads and the reads of a buffer precede its next stores; hipcc keeps the
@@ -868,23 +1009,41 @@ __device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, 
     if (S > 0 && together && wave_all(!valid || (reinterpret_cast<uintptr_t>(en.p) & 15u) == 0)) {
         fused_lane_stages_v<uint4>(en, S, h);
     } else if (S > 0) {  // scattered or not 16-byte aligned: shared loads (any alignment)
-        const u32x4u* src[8];
-        coop_sources<8>(A, group, lane, src);
-        // stage loads run ahead unconditionally (clamped to the last stage:
-        // a repeated read at the end, never past a chunk)
-        uint32_t v[32];
-        coop_load(src, 0, v);
-        coop_store(lds, v, lane);
-        coop_load(src, min(1u, S - 1u), v);
-        for (uint32_t s = 0; s < S; ++s) {
-            uint32_t cur[32];
-            wave_lds_order();  // stage s stored (previous iteration) -> read
-            coop_read(lds + (s & 1u) * kCoopStageBytes, lane, cur);
-            wave_lds_order();  // buffer (s+1)&1 was read last iteration -> store
-            coop_store(lds + ((s + 1u) & 1u) * kCoopStageBytes, v, lane);
-            coop_load(src, min(s + 2u, S - 1u), v);
-            coop_compress(cur, h);
+        // Block loads shared across the wave go straight to LDS
+        // (global_load_lds), four blocks ahead in five 4 KiB buffers; each
+        // lane then reads its own chunk's block back (coop4_read).  Round 4
+        // staged 128-byte stages through VGPRs (8 global loads + 8
+        // ds_write_b128 per stage) with one stage in flight: this wave IS its
+        // chunks' chain (alone on its SIMD at F = 4), so a scattered load that
+        // had not landed one stage (~4900 cycles) later stalled it, and a
+        // second register stage did not fit the mixed kernel's 256 VGPRs
+        // (65536 uniform chunks permuted: 11.4 ms against 10.1 in place).
+        const uint32_t K = 2u * S;
+        const uint8_t* p[4];
+        const uint32_t piece = ((lane & 3u) - (lane >> 4)) & 3u;
+#pragma unroll
+        for (uint32_t i = 0; i < 4; ++i) {
+            const uint32_t ej = group * 64u + 16u * i + (lane >> 2);
+            p[i] = fetch_entry(A, ej < A.n ? ej : group * 64u).p + 16u * piece;
         }
+        const uint32_t base = lds_addr(lds);
+        // blocks 0..3 in flight (past the bulk region: the last block again,
+        // a harmless repeat that keeps the count of loads in flight fixed)
+#pragma unroll
+        for (uint32_t d = 0; d < kCoopBlockBufs - 1u; ++d) glds_block(p, min(d, K - 1u), base + d * kCoopBlockBytes);
+        uint32_t b = 0;  // buffer of block k
+        for (uint32_t k = 0; k < K; ++k) {
+            asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // block k landed (blocks k+1..k+3 may not have)
+            uint32_t w[16];
+            coop4_read(lds + b * kCoopBlockBytes, lane, w);
+            const uint32_t bn = b == 0u ? kCoopBlockBufs - 1u : b - 1u;  // block k-1's buffer, read last trip
+            glds_block(p, min(k + kCoopBlockBufs - 1u, K - 1u), base + bn * kCoopBlockBytes);
+#pragma unroll
+            for (int j = 0; j < 16; ++j) w[j] = bswap_fresh(w[j]);
+            compress(h, w);
+            b = b + 1u == kCoopBlockBufs ? 0u : b + 1u;
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing of ours in flight past the loop
     }
     if (valid) {
         lane_blocks(A, en, 2u * S, h);

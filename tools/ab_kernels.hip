@@ -13,7 +13,7 @@
 
 namespace {
 constexpr int kStudyUnits[] = {2, 3, 20, 21, 24, 30, 31, 34, 44, 45, 504, 505, 569, 577, 585,
-                               8, 9, 10, 12, 13, 16, 17, 86, 87};
+                               8, 9, 10, 12, 13, 16, 17, 86, 87, 91, 92, 93, 94, 95, 96, 97, 98, 99, 81, 82};
 }
 
 bool split_unit_study_built(int u) {
@@ -48,6 +48,55 @@ hipError_t launch_split_study(const BatchArgs& A, int unit, hipStream_t st) {
     case 585:  // the product's case 4 with schedule reads in four bursts of 5
         hipLaunchKernelGGL((sha1_split_kernel<4, 1, (77 & ~kVRead10) | kVCoop, 2>), dim3(groups), dim3(256), 0,
                            st, A);
+        break;
+    // round 5: the product's uniform case 11 (lane-per-chunk producer loads)
+    // with the second pair's read bursts shifted (91), with two bursts of 10
+    // (92), and both (93)
+    case 91:
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, (kSplit8V & ~kVCoop) | kVPhase, 2>), dim3((groups + 1) / 2),
+                           dim3(512), 0, st, A);
+        break;
+    case 92:
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, (kSplit8V & ~kVCoop) | kVRead10, 2>), dim3((groups + 1) / 2),
+                           dim3(512), 0, st, A);
+        break;
+    case 93:
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, (kSplit8V & ~kVCoop) | kVRead10 | kVPhase, 2>),
+                           dim3((groups + 1) / 2), dim3(512), 0, st, A);
+        break;
+    case 94:  // one burst of 20, the second pair's at round 40
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, (kSplit8V & ~kVCoop) | kVRead20 | kVPhase, 2>),
+                           dim3((groups + 1) / 2), dim3(512), 0, st, A);
+        break;
+    case 95:  // 93 with the shared (coop) producer loads of ragged batches
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, kSplit8V | kVRead10 | kVPhase, 2>), dim3((groups + 1) / 2),
+                           dim3(512), 0, st, A);
+        break;
+    case 96:  // 94 with the shared producer loads
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, kSplit8V | kVRead20 | kVPhase, 2>), dim3((groups + 1) / 2),
+                           dim3(512), 0, st, A);
+        break;
+    // probes (consumer barrier-wait and loop cycles over the digests): the
+    // product's uniform case 11 (97), 93 (98), the config-2 case 4 (99)
+    case 97:
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, (kSplit8V & ~kVCoop) | kVProbe, 2>), dim3((groups + 1) / 2),
+                           dim3(512), 0, st, A);
+        break;
+    case 98:
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, (kSplit8V & ~kVCoop) | kVRead10 | kVPhase | kVProbe, 2>),
+                           dim3((groups + 1) / 2), dim3(512), 0, st, A);
+        break;
+    case 99:
+        hipLaunchKernelGGL((sha1_split_kernel<4, 1, kSplitV<4> | kVProbe, kSplitNProd<4>>), dim3(groups),
+                           dim3(256), 0, st, A);
+        break;
+    case 81:  // 10-read bursts at rounds 10/50 (first pair) and 30/70 (second)
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, (kSplit8V & ~kVCoop) | kVRead10 | kVPhase2, 2>),
+                           dim3((groups + 1) / 2), dim3(512), 0, st, A);
+        break;
+    case 82:  // 81 with the probe
+        hipLaunchKernelGGL((sha1_split_kernel<2, 2, (kSplit8V & ~kVCoop) | kVRead10 | kVPhase2 | kVProbe, 2>),
+                           dim3((groups + 1) / 2), dim3(512), 0, st, A);
         break;
     case 13:  // the product's case 11 with lane-per-chunk producer loads on any layout
         hipLaunchKernelGGL((sha1_split_kernel<2, 2, kSplit8V & ~kVCoop, 2>), dim3((groups + 1) / 2), dim3(512), 0,

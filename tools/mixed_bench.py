@@ -65,9 +65,12 @@ def main():
                     help="hash each chunk from 1..15 bytes past its (16-byte aligned) start, 16 bytes "
                          "shorter: no wave has all lanes 16-byte aligned (the per-lane load path)")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--lib", default=None, help="A/B: load this libsha1chunk.so (and its backend) instead")
     a = ap.parse_args()
     import torch
     pkg = importlib.import_module("congestion-control-with-bittorren_amd")
+    if a.lib:
+        pkg.sha1chunk.LIB_PATH = os.path.abspath(a.lib)
     torch.cuda.set_device(0)
     pkg.set_device(0)
     rows = []
