@@ -50,13 +50,16 @@
 #include "sha1_split.hpp"
 
 // The mixed planner's measured constants (us per block of a group of 64
-// chunks, see `Makespan model` below).
+// chunks, see `Makespan model` below).  The scattered fused shapes (S) were
+// re-measured in round 5 after their loads moved to LDS-DMA four blocks
+// ahead (1.408 -> 1.334, 2.661 -> 2.628; profiles/mixed_const_r05.jsonl);
+// the other constants measured within 2 % of these there.
 #define PLAN_SPLIT4 0.743
 #define PLAN_SPLIT8 0.860
 #define PLAN_FUSED4T 1.254
-#define PLAN_FUSED4S 1.408
+#define PLAN_FUSED4S 1.334
 #define PLAN_FUSED8T 2.502
-#define PLAN_FUSED8S 2.661
+#define PLAN_FUSED8S 2.628
 // The fused constants are measured with every CU running the fused shape
 // (tools/mixed_constants.sh).  In a mixed plan the fused workgroups share the
 // chip with split ones and run faster: fitted over the 26 forced split-head

@@ -977,6 +977,28 @@ __device__ __forceinline__ void glds_block(const uint8_t* const (&p)[4], uint32_
     for (int i = 0; i < 4; ++i) glds16(p[i] + 64ull * k, buf + 1024u * (uint32_t)i);
 }
 
+// Block k of the LDS-DMA fused loop: `cur` holds block k (its LDS read
+// issued during block k-1); block k+1's read is issued into `nxt` once its
+// DMA has landed, block k+4's DMA goes into block k-1's buffer (read during
+// block k-2, consumed during block k-1), then block k is compressed while
+// block k+1's read is in flight.  At the start of block k the DMAs of
+// blocks k+1..k+3 are outstanding (12 loads): vmcnt(8) retires block k+1.
+__device__ __forceinline__ void glds_stage_step(const uint8_t* const (&p)[4], uint32_t k, uint32_t K,
+                                                const uint8_t* lds, uint32_t base, uint32_t lane, uint32_t& b,
+                                                const uint32_t (&cur)[16], uint32_t (&nxt)[16],
+                                                uint32_t (&h)[5]) {
+    const uint32_t b1 = b + 1u == kCoopBlockBufs ? 0u : b + 1u;      // block k+1's buffer
+    const uint32_t bp = b == 0u ? kCoopBlockBufs - 1u : b - 1u;      // block k-1's buffer
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    coop4_read(lds + b1 * kCoopBlockBytes, lane, nxt);
+    glds_block(p, min(k + kCoopBlockBufs - 1u, K - 1u), base + bp * kCoopBlockBytes);
+    uint32_t w[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) w[j] = bswap_fresh(cur[j]);
+    compress(h, w);
+    b = b1;
+}
+
 // lds: this wave's kCoopWaveBytes.  Same contract as fused_body.  The
 // wave's LDS accesses complete in order, so a stage's stores precede its
 // reads and the reads of a buffer precede its next stores; hipcc keeps the
@@ -1031,18 +1053,16 @@ __device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, 
         // a harmless repeat that keeps the count of loads in flight fixed)
 #pragma unroll
         for (uint32_t d = 0; d < kCoopBlockBufs - 1u; ++d) glds_block(p, min(d, K - 1u), base + d * kCoopBlockBytes);
+        asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // block 0 landed
+        uint32_t wa[16], wb[16];
+        coop4_read(lds, lane, wa);
         uint32_t b = 0;  // buffer of block k
-        for (uint32_t k = 0; k < K; ++k) {
-            asm volatile("s_waitcnt vmcnt(12)" ::: "memory");  // block k landed (blocks k+1..k+3 may not have)
-            uint32_t w[16];
-            coop4_read(lds + b * kCoopBlockBytes, lane, w);
-            const uint32_t bn = b == 0u ? kCoopBlockBufs - 1u : b - 1u;  // block k-1's buffer, read last trip
-            glds_block(p, min(k + kCoopBlockBufs - 1u, K - 1u), base + bn * kCoopBlockBytes);
-#pragma unroll
-            for (int j = 0; j < 16; ++j) w[j] = bswap_fresh(w[j]);
-            compress(h, w);
-            b = b + 1u == kCoopBlockBufs ? 0u : b + 1u;
+        uint32_t k = 0;
+        for (; k + 1 < K; k += 2) {
+            glds_stage_step(p, k, K, lds, base, lane, b, wa, wb, h);
+            glds_stage_step(p, k + 1, K, lds, base, lane, b, wb, wa, h);
         }
+        if (k < K) glds_stage_step(p, k, K, lds, base, lane, b, wa, wb, h);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // nothing of ours in flight past the loop
     }
     if (valid) {

@@ -1,6 +1,8 @@
-# round-5 study session (split phase variants, probe, verify-queue submit stats)
+# round-5 study session: LDS-DMA fused loop, tests + A/B against the round-4 build
 set -u
-timeout -k 10 200 python tools/split_probe.py --lib congestion-control-with-bittorren_amd/build-ab/libsha1chunk.so --cases 97:32768,98:32768,82:32768 > gpurun_out/split_probe_r05c.log 2>&1 || exit 1
-timeout -k 10 600 python tools/sweep.py --lib congestion-control-with-bittorren_amd/build-ab/libsha1chunk.so --chunks 32768 --kernels split11,split93,split81 --rounds 6 --burst 6 > gpurun_out/phase_ab_r05c.log 2>&1 || exit 1
-for m in submit reserve; do SHA1CHUNK_VQ_STATS=1 timeout -k 10 120 tools/vq_zc_bench --mode $m --chunks 16384 --producers 4 --distinct 4096 >> gpurun_out/vq_stats_r05.log 2>&1 || exit 1; done
+timeout -k 10 400 python -u -m pytest tests/test_gpu_mixed.py tests/test_gpu_layouts.py tests/test_gpu_fuzz.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/pytest_glds2_r05.log 2>&1; rc=$?; tail -2 gpurun_out/pytest_glds2_r05.log; [ $rc -eq 0 ] || exit $rc
+for lib in congestion-control-with-bittorren_amd/libsha1chunk.so congestion-control-with-bittorren_amd/build-old/libsha1chunk.so; do
+  for lay in arrival shuffled shuffled_blocks4; do timeout -k 10 300 python tools/mixed_bench.py --lib $lib --chunks 65536 --uniform 524288 --reps 5 --layout $lay --modes plan0.0.4,plan0.0.8 2>&1 | grep "^{" | sed "s|^|$lib |" >> gpurun_out/glds2_ab_r05.log || exit 1; done
+  for lay in arrival sorted; do timeout -k 10 300 python tools/mixed_bench.py --lib $lib --chunks 131072 --reps 5 --layout $lay --modes auto,plan0.187.4 2>&1 | grep "^{" | sed "s|^|$lib |" >> gpurun_out/glds2_ab_r05.log || exit 1; done
+done
 echo done
