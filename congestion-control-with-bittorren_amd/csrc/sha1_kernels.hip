@@ -52,8 +52,11 @@
 // The mixed planner's measured constants (us per block of a group of 64
 // chunks, see `Makespan model` below).  The scattered fused shapes (S) were
 // re-measured in round 5 after their loads moved to LDS-DMA four blocks
-// ahead (1.408 -> 1.334, 2.661 -> 2.628; profiles/mixed_const_r05.jsonl);
-// the other constants measured within 2 % of these there.
+// ahead (1.408 -> 1.334, 2.661 -> 2.628; profiles/mixed_const_r05.jsonl).
+// The same run measured the split and together-fused shapes at 0.742,
+// 1.268 and 2.489 (within 1.2 % of these) and the 8-wave shape at 0.803,
+// 7 % under its constant; kept, as the 8-wave mode is 12-14 % behind the
+// best split-head plan at 131072 chunks either way.
 #define PLAN_SPLIT4 0.743
 #define PLAN_SPLIT8 0.860
 #define PLAN_FUSED4T 1.254
