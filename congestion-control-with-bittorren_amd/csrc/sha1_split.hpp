@@ -478,8 +478,24 @@ constexpr int kVCross = 256;
 // the W slot): one load instruction touches 16 or 8 chunks instead of 64
 // (see `shared loads`).
 constexpr int kVCoop = 8192;
+// Round-5 study flag: two 4-wave one-pair workgroups per CU (80 KiB of LDS
+// each, 2-block units, two producers) with roles taken from the SIMD each
+// wave landed on, so the two consumers sit on different SIMDs (0 and 2) and
+// the producers share SIMDs 1 and 3, as in the 8-wave layout, but each pair
+// has its own s_barrier.  Without the SIMD roles the dispatcher put both
+// consumers on one SIMD on many CUs (10.67 ms at 32768 chunks,
+// profiles/split_unit_ab_r03.json).  cu_turn(): a per-CU counter in device
+// memory orders the workgroups that land on one CU (its parity picks SIMD 0
+// or 2 for the consumer).
+constexpr int kVSimdRole = 8192 * 2;
+__device__ uint32_t g_cu_turn[4096];
+__device__ __forceinline__ uint32_t cu_turn(uint32_t hw) {
+    const uint32_t xcc = __builtin_amdgcn_s_getreg((3u << 11) | (0u << 6) | 20u) & 15u;  // HW_REG_XCC_ID
+    const uint32_t cu = (((xcc * 8u + ((hw >> 13) & 7u)) * 2u + ((hw >> 12) & 1u)) * 16u + ((hw >> 8) & 15u)) & 4095u;
+    return atomicAdd(&g_cu_turn[cu], 1u);
+}
 template <int PAIRS, int V, int NPROD>
-constexpr int kSplitThreads = (V & kVLayout8) ? 512 : 64 * PAIRS * (1 + NPROD) + ((V & kVSkipWave2) ? 64 : 0);
+constexpr int kSplitThreads = (V & kVLayout8) ? 512 : (V & kVSimdRole) ? 256 : 64 * PAIRS * (1 + NPROD) + ((V & kVSkipWave2) ? 64 : 0);
 // Why W+K matters: the consumer's x = e + W + K as a VOP3 v_add3 (K in an
 // SGPR or a VGPR alike) runs the one-wave round stream at ~4.98 cycles per
 // instruction, the VOP2 v_add on a shipped W+K at the 4-cycle issue floor
@@ -673,6 +689,34 @@ __device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uin
                       (PAIRS == 2 && U == NPROD && (V & kVLayout8) != 0),
                   "two producers: one stage (U = 4) or one block (U = 2, 8-wave layout) each per unit");
     int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    if constexpr ((V & kVSimdRole) != 0) {
+        // Roles by the SIMD each wave actually landed on (two 4-wave
+        // workgroups per CU, see kVSimdRole): the first workgroup of a CU
+        // puts its consumer on SIMD 0, the second on SIMD 2; producers on
+        // SIMDs 1 and 3; the wave on the other even SIMD leaves.  Every wave
+        // derives the same assignment from the table of all four waves'
+        // SIMDs, so exactly one consumer and two producers exist however
+        // the waves were placed.
+        static_assert(PAIRS == 1 && NPROD == 2 && U == 2, "SIMD roles: one pair, two producers, 2-block units");
+        uint32_t* slots = reinterpret_cast<uint32_t*>(lds);
+        const uint32_t hw = __builtin_amdgcn_s_getreg((31u << 11) | (0u << 6) | 4u);  // HW_REG_HW_ID, bits 0..31
+        if ((threadIdx.x & 63u) == 0) slots[1 + wave] = (hw >> 4) & 3u;
+        if (threadIdx.x == 0) slots[0] = cu_turn(hw);
+        __syncthreads();
+        const uint32_t cs = (__builtin_amdgcn_readfirstlane(slots[0]) & 1u) ? 2u : 0u;
+        int wc = -1, wi = -1;
+        for (int w = 0; w < 4; ++w)
+            if (wc < 0 && slots[1 + w] == cs) wc = w;
+        if (wc < 0) wc = 0;
+        for (int w = 0; w < 4; ++w)
+            if (wi < 0 && w != wc && slots[1 + w] == (cs ^ 2u)) wi = w;
+        if (wi < 0) wi = wc == 3 ? 2 : 3;
+        int rank = 0;  // producer index: order among the two remaining waves
+        for (int w = 0; w < wave; ++w) rank += (w != wc && w != wi) ? 1 : 0;
+        __syncthreads();  // the table is read before the ring is written
+        if (wave == wi) return;  // never joins a barrier
+        wave = wave == wc ? 0 : 1 + rank;
+    }
     if constexpr ((V & kVSkipWave2) != 0) {
         static_assert(NPROD == 2 && PAIRS == 1, "skip-wave layout is for two producers");
         if (wave == 2) return;  // never joins a barrier: an ended wave is not waited for

@@ -13,7 +13,7 @@
 
 namespace {
 constexpr int kStudyUnits[] = {2, 3, 20, 21, 24, 30, 31, 34, 44, 45, 504, 505, 569, 577, 585,
-                               8, 9, 10, 12, 13, 16, 17, 86, 87, 91, 92, 93, 94, 95, 96, 97, 98, 99, 81, 82};
+                               8, 9, 10, 12, 13, 16, 17, 86, 87, 91, 92, 93, 94, 95, 96, 97, 98, 99, 81, 82, 83, 84};
 }
 
 bool split_unit_study_built(int u) {
@@ -97,6 +97,14 @@ hipError_t launch_split_study(const BatchArgs& A, int unit, hipStream_t st) {
     case 82:  // 81 with the probe
         hipLaunchKernelGGL((sha1_split_kernel<2, 2, (kSplit8V & ~kVCoop) | kVRead10 | kVPhase2 | kVProbe, 2>),
                            dim3((groups + 1) / 2), dim3(512), 0, st, A);
+        break;
+    case 83:  // two 4-wave one-pair workgroups per CU, roles by SIMD (kVSimdRole)
+        hipLaunchKernelGGL((sha1_split_kernel<2, 1, kVWK | kVUnmask | kVSimdRole, 2>), dim3(groups), dim3(256), 0,
+                           st, A);
+        break;
+    case 84:  // 83 with 10-read bursts
+        hipLaunchKernelGGL((sha1_split_kernel<2, 1, kVWK | kVUnmask | kVSimdRole | kVRead10, 2>), dim3(groups),
+                           dim3(256), 0, st, A);
         break;
     case 13:  // the product's case 11 with lane-per-chunk producer loads on any layout
         hipLaunchKernelGGL((sha1_split_kernel<2, 2, kSplit8V & ~kVCoop, 2>), dim3((groups + 1) / 2), dim3(512), 0,
