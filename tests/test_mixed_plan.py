@@ -67,17 +67,17 @@ def test_config5_law_plans(n, mode, lo, hi):
 
 
 def test_simulation_rejects_late_long_fused_jobs():
-    """At 131072 chunks the bounds alone pick H = 257 (> C: the 257th split
-    group and the first long fused jobs start only when a CU frees); the
-    simulated dispatch puts that plan above 16 ms (measured 17.36 in round 2,
-    17.39 with H = 256 in round 4) and picks one near 14 (the 8-wave mode,
-    measured 14.16; round-4 constants, profiles/mixed_const_r04.jsonl)."""
+    """At 131072 chunks a split head of H = 257 (> C: the 257th split group
+    and the first long fused jobs start only when a CU frees) -- what the
+    bounds alone picked with the round-2 to round-4 constants -- simulates
+    above 16 ms (measured 17.36 in round 2, 17.39 with H = 256 in round 4);
+    the plan chosen is near 14 ms with no such head.  (With round 5's
+    scattered-fused constants the bounds alone pick H = 191.)"""
     lens = law(131072)
     (lb, m0, H0, F0), (B, P, L) = M.model_plan(lens, C, simulate=False)
-    assert (m0, H0, F0) == (0, 257, 4)
     assert M.sim_plan(B, C, 0, 257, 4, L) > 16000
     (est, m, H, F), _ = M.model_plan(lens, C)
-    assert est < 14500
+    assert est < 14500 and (m == 1 or H <= C), (est, m, H, F)
 
 
 def test_sorted_insertion_sim_is_greedy_list_scheduling():
