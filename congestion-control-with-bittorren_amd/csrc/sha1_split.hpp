@@ -346,14 +346,17 @@ __device__ __forceinline__ void coop4_read(const uint8_t* buf, uint32_t lane, ui
 // Per-lane source pointers of the shared-load pattern with `lanes` lanes per
 // chunk: slot i is chunk group*64 + (64/lanes)*i + lane/lanes, piece
 // lane%lanes; a slot past the batch reads the group's first chunk (valid,
-// and at least as long as the wave's bulk region).
+// and at least as long as the wave's bulk region).  A group wholly past the
+// batch (the second pair of a split workgroup when the group count is odd)
+// takes the batch's last entry instead: never group*64, which indexes past
+// A.order, and its blocks are never loaded (no bulk region).
 template <int LANES>
 __device__ __forceinline__ void coop_sources(const BatchArgs& A, uint32_t group, uint32_t lane,
                                              const u32x4u* (&src)[LANES]) {
 #pragma unroll
     for (uint32_t i = 0; i < (uint32_t)LANES; ++i) {
         const uint32_t ej = group * 64u + (64u / LANES) * i + lane / LANES;
-        src[i] = reinterpret_cast<const u32x4u*>(fetch_entry(A, ej < A.n ? ej : group * 64u).p) + (lane % LANES);
+        src[i] = reinterpret_cast<const u32x4u*>(fetch_entry(A, ej < A.n ? ej : min(group * 64u, A.n - 1u)).p) + (lane % LANES);
     }
 }
 
@@ -1090,7 +1093,7 @@ __device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, 
 #pragma unroll
         for (uint32_t i = 0; i < 4; ++i) {
             const uint32_t ej = group * 64u + 16u * i + (lane >> 2);
-            p[i] = fetch_entry(A, ej < A.n ? ej : group * 64u).p + 16u * piece;
+            p[i] = fetch_entry(A, ej < A.n ? ej : min(group * 64u, A.n - 1u)).p + 16u * piece;
         }
         const uint32_t base = lds_addr(lds);
         // blocks 0..3 in flight (past the bulk region: the last block again,
