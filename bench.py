@@ -646,7 +646,10 @@ def _mixed_run(pkg, torch, lens: np.ndarray, reps: int = 5, warm: int = 2, layou
     if layout == "arrival":
         off, total = pkg.sha1chunk.ragged_layout(lens)
     else:
-        order = np.argsort(-lens.astype(np.int64), kind="stable")
+        # the device's order: descending SHA-1 block counts, stable
+        # (sha1_sort.hip), so every sorted group's chunks lie together
+        keys = np.minimum((lens.astype(np.int64) + 9 + 63) // 64, 65535)
+        order = np.argsort(-keys, kind="stable")
         o2, total = pkg.sha1chunk.ragged_layout(lens[order])
         off = np.empty_like(o2)
         off[order] = o2

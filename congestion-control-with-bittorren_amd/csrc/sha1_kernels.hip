@@ -383,6 +383,21 @@ __global__ __launch_bounds__(kLayoutThreads) void plan_layout_kernel(BatchArgs A
     const uint32_t lane = threadIdx.x % 64u, wave = threadIdx.x / 64u;
     const uint32_t G = (A.n + 63u) / 64u;
     __shared__ uint32_t tog[32], blk[32];
+    // The wave's groups' entries first, all in flight together: each is two
+    // dependent global reads (order, then offset and length), and taking
+    // the groups one at a time cost ~17 us at 2048 groups.
+    Entry en[kLayoutGroupsPerWave];
+#pragma unroll
+    for (uint32_t k = 0; k < kLayoutGroupsPerWave; ++k) {
+        const uint32_t e = 64u * (32u * blockIdx.x + wave * kLayoutGroupsPerWave + k) + lane;
+        if (e < A.n) {
+            en[k] = fetch_entry(A, e);
+        } else {
+            en[k].p = nullptr;
+            en[k].len = 0;
+        }
+    }
+#pragma unroll
     for (uint32_t k = 0; k < kLayoutGroupsPerWave; ++k) {
         const uint32_t slot = wave * kLayoutGroupsPerWave + k;
         const uint32_t g = 32u * blockIdx.x + slot;
@@ -393,10 +408,9 @@ __global__ __launch_bounds__(kLayoutThreads) void plan_layout_kernel(BatchArgs A
         const uint32_t e = 64u * g + lane;
         uint64_t lo = ~0ull, hi = 0, bytes = 0;
         if (e < A.n) {
-            const Entry en = fetch_entry(A, e);
-            lo = reinterpret_cast<uint64_t>(en.p);
-            hi = lo + en.len;
-            bytes = en.len;
+            lo = reinterpret_cast<uint64_t>(en[k].p);
+            hi = lo + en[k].len;
+            bytes = en[k].len;
         }
 #pragma unroll
         for (uint32_t m = 1; m < 64; m *= 2) {
@@ -492,27 +506,47 @@ __device__ __forceinline__ uint32_t plan_jobs(uint32_t G, uint32_t mode, uint32_
     return mode == 1 ? (G + 1u) / 2u : H + (G - H + F - 1u) / F;
 }
 
-__device__ __forceinline__ float sim_job(const uint32_t* blocks, const PlanLayout& L, uint32_t G, uint32_t mode,
-                                         uint32_t H, uint32_t F, uint32_t j) {
-    if (mode == 1) return (float)blocks[2u * j] * kChainSplit8f;
-    if (j < H) return (float)blocks[j] * kChainSplit4f;
-    const uint32_t g = H + (j - H) * F;
-    const bool t = L.job_together(g, F, G);
-    return (float)blocks[g] * (F == 4 ? (t ? kChainFused4Tf : kChainFused4Sf) : (t ? kChainFused8Tf : kChainFused8Sf));
+// Job j's first group (the one whose blocks set its duration).
+__device__ __forceinline__ uint32_t sim_group(uint32_t mode, uint32_t H, uint32_t F, uint32_t j) {
+    return mode == 1 ? 2u * j : (j < H ? j : H + (j - H) * F);
+}
+
+// Job j's duration from its group's blocks and run (both read one job ahead
+// by sim_xcd), branch-free: the lanes of a wave simulate different
+// candidates, and a per-mode branch with its own LDS read and wait on each
+// path cost ~3x the job's VALU (round 4's form; the fp32 product is the
+// same, so are the times).
+__device__ __forceinline__ float sim_dur(uint32_t mode, uint32_t H, uint32_t F, uint32_t j, uint32_t b, uint32_t r) {
+#pragma clang fp contract(off)  // rounded here, never fused into the insert's add (the model's order)
+    const float ft = F == 4 ? (r >= 4u ? kChainFused4Tf : kChainFused4Sf) : (r >= 8u ? kChainFused8Tf : kChainFused8Sf);
+    const float c = mode == 1 ? kChainSplit8f : (j < H ? kChainSplit4f : ft);
+    return (float)b * c;
 }
 
 // Jobs x, x + 8, .. of a plan on one XCD's `per` CUs: the time its last CU
 // frees.  t holds the free times in ascending order (+inf past `per`); a
-// job starts at t[0] and its end is inserted in order.
+// job starts at t[0] and its end is inserted in order.  Simulated only for
+// G <= kSimMaxG, so every job's group has its blocks and run in LDS.
 __device__ float sim_xcd(const uint32_t* blocks, const PlanLayout& L, uint32_t G, uint32_t mode, uint32_t H,
                          uint32_t F, uint32_t x, uint32_t per) {
     float t[kSimCus];
 #pragma unroll
     for (uint32_t i = 0; i < kSimCus; ++i) t[i] = i < per ? 0.0f : __builtin_inff();
     const uint32_t J = plan_jobs(G, mode, H, F);
-#pragma unroll 4
+    uint32_t b = 0, r = 0;
+    if (x < J) {
+        const uint32_t g = sim_group(mode, H, F, x);
+        b = blocks[g];
+        r = L.run[g];
+    }
     for (uint32_t j = x; j < J; j += kSimXcds) {
-        const float nx = t[0] + sim_job(blocks, L, G, mode, H, F, j);
+        const float d = sim_dur(mode, H, F, j, b, r);
+        if (j + kSimXcds < J) {  // the next job's reads, in flight during this insert
+            const uint32_t g = sim_group(mode, H, F, j + kSimXcds);
+            b = blocks[g];
+            r = L.run[g];
+        }
+        const float nx = t[0] + d;
         // t ascending: the new t[i] is nx clamped to [t[i], t[i+1]]
 #pragma unroll
         for (uint32_t i = 0; i + 1 < kSimCus; ++i) t[i] = __builtin_amdgcn_fmed3f(t[i], nx, t[i + 1]);

@@ -710,6 +710,30 @@ int s1be_hash_uniform_async(const void* d_base, uint32_t chunk_len, size_t n,
     return launch_checked(choose_kernel(kernel, n, D->cus), A, static_cast<hipStream_t>(stream), D->cus);
 }
 
+// Diagnostics (tests; no frontend entry point): the longest-first order and
+// sorted lengths AUTO's ragged path hashes a batch of lengths in
+// (sha1_sort.hip), copied into the caller's device arrays of n entries.
+int s1be_sort_order_async(const uint32_t* d_lengths, size_t n, uint32_t* d_order, uint32_t* d_sorted_len,
+                          void* stream) {
+    if (n > 0xffffffffu) return fail(SHA1CHUNK_EINVAL, "n too large");
+    if (n == 0) return SHA1CHUNK_OK;
+    if (!d_lengths || !d_order || !d_sorted_len) return fail(SHA1CHUNK_EINVAL, "null device pointer");
+    Device* D;
+    if (int rc = get_device(&D)) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const uint32_t *order = nullptr, *sorted_len = nullptr;
+    uint32_t* plan = nullptr;
+    void* scratch = nullptr;
+    hipError_t e = sort_by_length_desc(d_lengths, static_cast<uint32_t>(n), &order, &sorted_len, &plan, &scratch, st);
+    if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "length sort: %s", hipGetErrorString(e));
+    e = hipMemcpyAsync(d_order, order, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(d_sorted_len, sorted_len, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
+    (void)hipFreeAsync(scratch, st);
+    if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "sort copy: %s", hipGetErrorString(e));
+    return SHA1CHUNK_OK;
+}
+
 int s1be_compare_device_async(const uint8_t* d_digests, const uint8_t* d_expected, size_t n,
                                    uint8_t* d_mismatch, void* stream) {
     if (n > 0xffffffffu) return fail(SHA1CHUNK_EINVAL, "n too large");

@@ -181,7 +181,9 @@ def model_plan(lengths, C, simulate=True, offsets=None):
     if offsets is None:
         offsets = np.zeros(lengths.size, np.int64)
         offsets[1:] = np.cumsum((lengths + 63) // 64 * 64)[:-1]
-    order = np.argsort(-lengths, kind="stable")  # the device's stable radix sort
+    # the device's order (sha1_sort.hip): descending block counts, clamped
+    # at 65535, ties in caller order
+    order = np.argsort(-np.minimum((lengths + 9 + 63) // 64, 65535), kind="stable")
     srt = lengths[order]
     B = [int(b) for b in total_blocks(srt[::64])]
     G = len(B)

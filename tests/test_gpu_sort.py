@@ -1,0 +1,92 @@
+"""The longest-first order AUTO hashes a ragged batch in (sha1_sort.hip):
+descending SHA-1 block counts, ceil((len + 9) / 64) clamped at 65535, ties
+in caller order -- numpy's stable argsort of the same keys, position for
+position, and the sorted lengths the planner reads.  Tile edges of the
+three-kernel radix sort (4096 chunks), all-equal and all-distinct keys,
+empty chunks, chunks of 4 MiB and more (clamped keys tie), and the rocPRIM
+path beyond 1 Mi chunks.  Through the backend's diagnostics entry point
+s1be_sort_order_async (no frontend symbol)."""
+import ctypes as C
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG_DIR = os.path.join(ROOT, "congestion-control-with-bittorren_amd")
+
+
+@pytest.fixture(scope="module")
+def sort_order(pkg):
+    import torch
+    assert torch.cuda.is_available(), "GPU tests need a device"
+    torch.cuda.set_device(0)
+    pkg.set_device(0)
+    be = C.CDLL(os.path.join(PKG_DIR, "libsha1chunk_hip.so"))
+    f = be.s1be_sort_order_async
+    f.restype = C.c_int
+    f.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p]
+
+    def run(lens):
+        n = lens.size
+        d_len = torch.from_numpy(lens.astype(np.int32)).cuda()
+        d_ord = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        d_srt = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        rc = f(d_len.data_ptr(), n, d_ord.data_ptr(), d_srt.data_ptr(), None)
+        assert rc == 0, rc
+        torch.cuda.synchronize()
+        return d_ord.cpu().numpy().view(np.uint32), d_srt.cpu().numpy().view(np.uint32)
+
+    return run
+
+
+def keys(lens):
+    return np.minimum((lens.astype(np.int64) + 9 + 63) // 64, 65535)
+
+
+def want(lens):
+    return np.argsort(-keys(lens), kind="stable").astype(np.uint32)
+
+
+def check(sort_order, lens):
+    order, srt = sort_order(lens)
+    w = want(lens)
+    bad = np.flatnonzero(order != w)
+    assert bad.size == 0, (lens.size, bad[:8], order[bad[:8]], w[bad[:8]])
+    assert np.array_equal(srt, lens[w].astype(np.uint32))
+
+
+@pytest.mark.parametrize("n", [65, 4095, 4096, 4097, 8192 + 63, 131072, 262144 + 4093])
+def test_config5_law_and_tile_edges(sort_order, n):
+    rng = np.random.default_rng(n)
+    lens = np.exp(rng.uniform(np.log(4096), np.log(1 << 20), n)).astype(np.uint32)
+    lens[rng.choice(n, min(n, 40), replace=False)] = 0
+    lens[rng.choice(n, min(n, 40), replace=False)] = 55   # 1 block
+    lens[rng.choice(n, min(n, 40), replace=False)] = 56   # 2 blocks
+    check(sort_order, lens)
+
+
+def test_ties_and_clamp(sort_order):
+    """Few distinct keys (long runs of ties across tiles, both digits), and
+    chunks of 4 MiB and more whose keys clamp to 65535 (caller order)."""
+    rng = np.random.default_rng(5)
+    n = 50000
+    lens = rng.choice(np.array([0, 64, 119, 120, 183, 184, 4096, 65536 * 64, (1 << 22) - 9, 1 << 22, 1 << 30],
+                               dtype=np.uint64), n).astype(np.uint32)
+    check(sort_order, lens)
+    check(sort_order, np.full(9000, 1000, np.uint32))              # one key
+    check(sort_order, np.arange(70000, dtype=np.uint32) * 64)      # every key distinct-ish, ascending
+    check(sort_order, (np.arange(70000, dtype=np.uint32)[::-1] * 64).copy())  # already sorted
+
+
+def test_rocprim_path_beyond_1mi(sort_order):
+    """Past 256 tiles of 4096 the same keys go through rocPRIM's onesweep:
+    the same order."""
+    rng = np.random.default_rng(11)
+    n = (1 << 20) + 4097
+    lens = rng.integers(0, 300000, n).astype(np.uint32)
+    lens[rng.choice(n, 1000, replace=False)] = 1 << 23
+    check(sort_order, lens)
