@@ -375,7 +375,7 @@ __device__ __forceinline__ uint32_t plan_blocks(const uint32_t* sorted_len, cons
 // ~0.5 ms at 262144 chunks).  Workgroup w summarises groups 32w .. 32w+31:
 // bits[w] (bit i: group 32w+i lies together) and tb[w] (the blocks of those
 // groups, the planner's together share).
-constexpr int kLayoutThreads = 256;
+constexpr int kLayoutThreads = 1024;  // two groups per wave (eight at 256 threads: 16.5 us at 2048 groups)
 constexpr uint32_t kLayoutGroupsPerWave = 32 / (kLayoutThreads / 64);
 
 __global__ __launch_bounds__(kLayoutThreads) void plan_layout_kernel(BatchArgs A, const uint32_t* sorted_len,
@@ -506,57 +506,68 @@ __device__ __forceinline__ uint32_t plan_jobs(uint32_t G, uint32_t mode, uint32_
     return mode == 1 ? (G + 1u) / 2u : H + (G - H + F - 1u) / F;
 }
 
-// Job j's first group (the one whose blocks set its duration).
-__device__ __forceinline__ uint32_t sim_group(uint32_t mode, uint32_t H, uint32_t F, uint32_t j) {
-    return mode == 1 ? 2u * j : (j < H ? j : H + (j - H) * F);
-}
-
-// Job j's duration from its group's blocks and run (both read one job ahead
-// by sim_xcd), branch-free: the lanes of a wave simulate different
-// candidates, and a per-mode branch with its own LDS read and wait on each
-// path cost ~3x the job's VALU (round 4's form; the fp32 product is the
-// same, so are the times).
-__device__ __forceinline__ float sim_dur(uint32_t mode, uint32_t H, uint32_t F, uint32_t j, uint32_t b, uint32_t r) {
-#pragma clang fp contract(off)  // rounded here, never fused into the insert's add (the model's order)
-    const float ft = F == 4 ? (r >= 4u ? kChainFused4Tf : kChainFused4Sf) : (r >= 8u ? kChainFused8Tf : kChainFused8Sf);
-    const float c = mode == 1 ? kChainSplit8f : (j < H ? kChainSplit4f : ft);
-    return (float)b * c;
+// v_med3_u32 (no builtin for the unsigned form); volatile, so the LDS
+// reads sim_xcd issues ahead of an insert stay ahead of it.
+__device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t r;
+    asm volatile("v_med3_u32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
 }
 
 // Jobs x, x + 8, .. of a plan on one XCD's `per` CUs: the time its last CU
 // frees.  t holds the free times in ascending order (+inf past `per`); a
 // job starts at t[0] and its end is inserted in order.  Simulated only for
 // G <= kSimMaxG, so every job's group has its blocks and run in LDS.
+//
+// Job j runs group g_j: split jobs (j < Hs) g = m*j (m = 2 for the 8-wave
+// mode's pairs), fused jobs g = Hs + (j - Hs)*F; its duration is the
+// group's blocks times the shape's chain constant (fused: by whether the F
+// groups from g lie together), the fp32 product rounded before the add
+// (contract off; tests/test_gpu_mixed.py restates it bit for bit).
+// Branch-free, with the next job's two LDS reads in flight during this
+// job's insert: the lanes of a wave simulate different candidates, and a
+// per-mode branch with its own read and wait (round 4) cost ~3x this.
 __device__ float sim_xcd(const uint32_t* blocks, const PlanLayout& L, uint32_t G, uint32_t mode, uint32_t H,
                          uint32_t F, uint32_t x, uint32_t per) {
-    float t[kSimCus];
+#pragma clang fp contract(off)
+    typedef const volatile __attribute__((address_space(3))) uint32_t lds_u32;
+    typedef const volatile __attribute__((address_space(3))) uint8_t lds_u8v;
+    // Free times as the bits of non-negative floats, which order as
+    // unsigned integers (+inf above every finite time), so the insert is
+    // v_med3_u32: ~205 shader cycles per job against ~300 for v_med3_f32 and
+    // ~400 for v_min_u32 + v_max_u32 pairs (one wave, tools/insert_probe.hip,
+    // profiles/insert_probe_r05.log).
+    uint32_t t[kSimCus];
 #pragma unroll
-    for (uint32_t i = 0; i < kSimCus; ++i) t[i] = i < per ? 0.0f : __builtin_inff();
+    for (uint32_t i = 0; i < kSimCus; ++i) t[i] = i < per ? 0u : 0x7f800000u;
     const uint32_t J = plan_jobs(G, mode, H, F);
+    const uint32_t Hs = mode == 1 ? J : H, m = mode == 1 ? 2u : 1u;
+    const float cs = mode == 1 ? kChainSplit8f : kChainSplit4f;
+    const float cT = F == 8 ? kChainFused8Tf : kChainFused4Tf, cS = F == 8 ? kChainFused8Sf : kChainFused4Sf;
+    auto group = [&](uint32_t j) { return j < Hs ? m * j : Hs + (j - Hs) * F; };
     uint32_t b = 0, r = 0;
     if (x < J) {
-        const uint32_t g = sim_group(mode, H, F, x);
-        b = blocks[g];
-        r = L.run[g];
+        const uint32_t g = group(x);
+        b = *(lds_u32*)(&blocks[g]);
+        r = *(lds_u8v*)(&L.run[g]);
     }
     for (uint32_t j = x; j < J; j += kSimXcds) {
-        const float d = sim_dur(mode, H, F, j, b, r);
-        if (j + kSimXcds < J) {  // the next job's reads, in flight during this insert
-            const uint32_t g = sim_group(mode, H, F, j + kSimXcds);
-            b = blocks[g];
-            r = L.run[g];
-        }
-        const float nx = t[0] + d;
+        const float c = j < Hs ? cs : (r >= F ? cT : cS);
+        const float d = (float)b * c;
+        const uint32_t g = group(j + kSimXcds < J ? j + kSimXcds : j);  // the next job (this one past the end)
+        b = *(lds_u32*)(&blocks[g]);
+        r = *(lds_u8v*)(&L.run[g]);
+        const uint32_t nx = __float_as_uint(__uint_as_float(t[0]) + d);
         // t ascending: the new t[i] is nx clamped to [t[i], t[i+1]]
 #pragma unroll
-        for (uint32_t i = 0; i + 1 < kSimCus; ++i) t[i] = __builtin_amdgcn_fmed3f(t[i], nx, t[i + 1]);
-        t[kSimCus - 1] = fmaxf(t[kSimCus - 1], nx);
+        for (uint32_t i = 0; i + 1 < kSimCus; ++i) t[i] = umed3(t[i], nx, t[i + 1]);
+        t[kSimCus - 1] = max(t[kSimCus - 1], nx);
     }
-    float last = 0.0f;
+    uint32_t last = 0u;
 #pragma unroll
     for (uint32_t i = 0; i < kSimCus; ++i)
-        if (i < per) last = fmaxf(last, t[i]);
-    return last;
+        if (i < per) last = max(last, t[i]);
+    return __uint_as_float(last);
 }
 
 // One workgroup, two stages.  Bounds: every mode-0 plan (H in [0, hcap] or
@@ -583,7 +594,12 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     // stage end times (s_memrealtime, 100 MHz; plan[8..13], thread 0) for
     // SHA1CHUNK_MIXED_DEBUG: scan, bounds search, passes 1, 2, 3
     uint64_t ts[6] = {0, 0, 0, 0, 0, 0};
-    if (t == 0) ts[0] = __builtin_amdgcn_s_memrealtime();
+    // and the shader-clock cycles at the same points (plan[14..18])
+    uint64_t cs[6] = {0, 0, 0, 0, 0, 0};
+    if (t == 0) {
+        ts[0] = __builtin_amdgcn_s_memrealtime();
+        cs[0] = __builtin_amdgcn_s_memtime();
+    }
     if (forced) {
         if (t == 0) {
             plan[0] = fmode;
@@ -626,7 +642,10 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     }
     const uint64_t PG = scan[kPlanThreads - 1];
     const double ft = PG ? (double)tog_blocks / (double)PG : 1.0;
-    if (t == 0) ts[1] = __builtin_amdgcn_s_memrealtime();
+    if (t == 0) {
+        ts[1] = __builtin_amdgcn_s_memrealtime();
+        cs[1] = __builtin_amdgcn_s_memtime();
+    }
     __shared__ uint8_t run8[kSimMaxG];
     for (uint32_t g = t; g < min(G, kSimMaxG); g += kPlanThreads) {
         uint32_t r = 0;
@@ -673,7 +692,10 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         }
         __syncthreads();
     }
-    if (t == 0) ts[2] = __builtin_amdgcn_s_memrealtime();
+    if (t == 0) {
+        ts[2] = __builtin_amdgcn_s_memrealtime();
+        cs[2] = __builtin_amdgcn_s_memtime();
+    }
     const bool simulate = G <= kSimMaxG && cus % kSimXcds == 0 && cus / kSimXcds <= kSimCus;
     if (!simulate) {
         if (t == 0) {
@@ -686,58 +708,119 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         }
         return;
     }
-    // Candidates: the bounds' best plan, the 8-wave mode, all-split, split
-    // heads around the bounds' best, and a grid of heads up to 2C (both F).
+    // Candidates, in the order every pass and the final choice index them
+    // (tests/test_gpu_mixed.py candidates()): 0 the bounds' best plan, 1 the
+    // 8-wave mode, 2 all-split, then heads hb - d, hb + d for d = 1, 2, 4 ..
+    // 64 while in range (only H <= hcap: prefix[] holds P_H there -- when
+    // the best is all-split beyond hcap, hb - d would be neither a searched
+    // head nor all-split), then a grid of 32 heads up to 2C at F = 4 and,
+    // below G, 8.  Wave 0 builds the list in parallel (positions from
+    // ballots), then each candidate's makespan bounds are computed once.
     constexpr uint32_t kMaxCand = kPlanThreads / kSimXcds;
-    __shared__ uint32_t cmode[kMaxCand], chead[kMaxCand], cf[kMaxCand], ncand;
+    constexpr uint32_t kSpec = 16, kSpec0 = kMaxCand - kSpec;  // heads hb -/+ 1..8 simulated ahead
+    __shared__ uint32_t cmode[kMaxCand], chead[kMaxCand], cf[kMaxCand], ncand, nref, npend, nmiss;
     __shared__ float cmk[kMaxCand];
-    if (t == 0) {
-        uint32_t k = 0;
-        auto add = [&](uint32_t m, uint32_t h, uint32_t f) {
-            cmode[k] = m;
-            chead[k] = h;
-            cf[k] = h == G ? 4u : f;
-            ++k;
-        };
-        const uint32_t hb = best_h[0], fb = best_f[0];
-        add(0, hb, fb);
-        add(1, 0, 0);
-        add(0, G, 4);
-        // heads below the bounds' best; only H <= hcap (prefix[] holds P_H
-        // there) -- when the best is all-split beyond hcap, hb - d would be
-        // neither a searched head nor all-split
-        for (uint32_t d = 1; d <= 64; d *= 2) {
-            if (hb >= d && hb - d <= hcap) add(0, hb - d, fb);
-            if (hb + d <= hcap) add(0, hb + d, fb);
+    __shared__ double clb[kMaxCand];
+    __shared__ uint8_t cstate[kMaxCand], sval[kSpec];
+    const uint32_t hb = best_h[0], fb = best_f[0];
+    const double mb = best_m[0];
+    auto put = [&](uint32_t k, uint32_t m, uint32_t h, uint32_t f) {
+        cmode[k] = m;
+        chead[k] = h;
+        cf[k] = h == G ? 4u : f;
+    };
+    if (t < kMaxCand) cstate[t] = 0;
+    if (t < 64) {
+        // lanes 0..13: the d entries (lane 2q: hb - 2^q, 2q + 1: hb + 2^q);
+        // lanes 14..45: grid head i = lane - 14 (at F = 4, and 8 below G)
+        uint32_t cnt = 0, h0 = 0, f0 = 0;
+        if (t < 14) {
+            const uint32_t d = 1u << (t >> 1);
+            if ((t & 1u) == 0u ? (hb >= d && hb - d <= hcap) : (hb + d <= hcap)) {
+                cnt = 1;
+                h0 = (t & 1u) == 0u ? hb - d : hb + d;
+                f0 = fb;
+            }
+        } else if (t < 46) {
+            h0 = (t - 14u) * min(hcap, 2u * cus) / 31u;
+            f0 = 4;
+            cnt = h0 < G ? 2u : 1u;
         }
-        const uint32_t top = min(hcap, 2u * cus);
-        for (uint32_t i = 0; i < 32; ++i) {
-            const uint32_t h = i * top / 31u;
-            add(0, h, 4);
-            if (h < G) add(0, h, 8);
+        const uint64_t below = (1ull << t) - 1ull;
+        const uint32_t pos = 3u + __popcll(__ballot(cnt >= 1u) & below) + __popcll(__ballot(cnt == 2u) & below);
+        if (cnt >= 1u) put(pos, 0, h0, f0);
+        if (cnt == 2u) put(pos + 1u, 0, h0, 8);
+        if (t == 0) {
+            put(0, 0, hb, fb);
+            put(1, 1, 0, 0);
+            put(2, 0, G, 4);
+            npend = 0;
+            nmiss = 0;
         }
-        ncand = k;
+        if (t == 63) ncand = pos + cnt;
+    } else if (t < 64 + kSpec) {
+        // pass 3's heads if the bounds' best stays the best split-head plan
+        const uint32_t q = t - 64u, d = q / 2u + 1u;
+        const bool ok = hb < G && ((q & 1u) == 0u ? hb >= d : (hb + d <= hcap && hb + d < G));
+        sval[q] = ok ? 1 : 0;
+        put(kSpec0 + q, 0, (q & 1u) == 0u ? hb - d : hb + d, fb);
+    }
+    __syncthreads();
+    if (t >= 1 && t < ncand) {
+        const uint32_t m = cmode[t], h = chead[t], f = cf[t];
+        clb[t] = m == 1 ? makespan(sorted_len, blocks, L, ft, G, cus, 1, 0, 0, 0, PG)
+                        : makespan(sorted_len, blocks, L, ft, G, cus, 0, h, f, h <= hcap ? prefix[h] : PG, PG);
     }
     __syncthreads();
     // Pass 1 simulates the bounds' plan; pass 2 every other candidate whose
     // bounds are below that time (the rest cannot beat it; a 4096-group
-    // all-split candidate alone is ~100 us of simulation).
-    const uint32_t c = t / kSimXcds, x = t % kSimXcds;
-    for (uint32_t pass = 0; pass < 2; ++pass) {
-        bool run = pass == 0 ? c == 0 : (c >= 1 && c < ncand);
-        if (run && pass == 1) {
-            const uint32_t m = cmode[c], h = chead[c], f = cf[c];
-            const double lb = m == 1 ? makespan(sorted_len, blocks, L, ft, G, cus, 1, 0, 0, 0, PG)
-                                     : makespan(sorted_len, blocks, L, ft, G, cus, 0, h, f, h <= hcap ? prefix[h] : PG, PG);
-            run = lb < (double)cmk[0];
-        }
+    // all-split candidate alone is ~100 us of simulation); pass 3 the heads
+    // next to the best split-head plan after pass 2.  Simulating is the
+    // same for every candidate whenever it runs, so the first sweep takes
+    // the bounds' plan, every candidate whose bounds are within 5 % of it
+    // (pass 2's usual survivors) and pass 3's heads as they would be if the
+    // bounds' best stays the best split head; pass 2's rest and pass 3's
+    // misses follow only if needed.  Each sweep is the longest candidate's
+    // chain of inserts, so this is one sweep instead of three in the usual
+    // case.  The choice is the same as passes 1-3 in order.
+    const uint32_t c = t / kSimXcds, x = t % kSimXcds, xcus = cus / kSimXcds;
+    const double early = mb * 1.05;
+    {
+        const bool run = c == 0 || (c < ncand && clb[c] < early) || (c >= kSpec0 && sval[c - kSpec0]);
         float mk = __builtin_inff();
-        if (run) mk = sim_xcd(blocks, L, G, cmode[c], chead[c], cf[c], x, cus / kSimXcds);
+        if (run) mk = sim_xcd(blocks, L, G, cmode[c], chead[c], cf[c], x, xcus);
 #pragma unroll
         for (uint32_t m = 1; m < kSimXcds; m *= 2) mk = fmaxf(mk, __shfl_xor(mk, m));
-        if (x == 0 && (pass == 0 ? c == 0 : c >= 1)) cmk[c] = mk;
+        if (x == 0 && run) cmk[c] = mk;
         __syncthreads();
-        if (t == 0) ts[3 + pass] = __builtin_amdgcn_s_memrealtime();
+        if (t == 0) {
+            ts[3] = __builtin_amdgcn_s_memrealtime();
+            cs[3] = __builtin_amdgcn_s_memtime();
+        }
+    }
+    // pass 2's rule: bounds at or above the bounds' plan's simulated time
+    // rule a candidate out (cmk = inf, simulated early or not)
+    if (t >= 1 && t < ncand) {
+        if (!(clb[t] < (double)cmk[0])) {
+            cmk[t] = __builtin_inff();
+        } else if (!(clb[t] < early)) {
+            cstate[t] = 1;
+            atomicAdd(&npend, 1u);
+        }
+    }
+    __syncthreads();
+    if (npend) {
+        const bool run = c < ncand && cstate[c] == 1;
+        float mk = __builtin_inff();
+        if (run) mk = sim_xcd(blocks, L, G, cmode[c], chead[c], cf[c], x, xcus);
+#pragma unroll
+        for (uint32_t m = 1; m < kSimXcds; m *= 2) mk = fmaxf(mk, __shfl_xor(mk, m));
+        if (x == 0 && run) cmk[c] = mk;
+        __syncthreads();
+    }
+    if (t == 0) {
+        ts[4] = __builtin_amdgcn_s_memrealtime();
+        cs[4] = __builtin_amdgcn_s_memtime();
     }
     // Pass 3: heads next to the shortest split-head plan so far (same F;
     // whichever plan is shortest overall).  The simulated
@@ -745,42 +828,48 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     // neighbours by several percent (config-5 law at 131072 chunks in
     // arrival order: H = 187 simulated 13.88 ms and measured 13.92, mode 1
     // 14.09 / 14.27, H = 176 14.35 / 14.41) and the grid above steps ~16
-    // heads, so every head within 8 of the best split-head plan is tried.
-    __shared__ uint32_t nref;
+    // heads, so every head within 8 of the best split-head plan is tried
+    // (taken from the first sweep when it simulated that head).
     if (t == 0) {
         uint32_t bi = kMaxCand;  // the shortest mode-0 candidate with a fused tail
         for (uint32_t i = 0; i < ncand; ++i)
             if (cmode[i] == 0 && chead[i] < G && (bi == kMaxCand || cmk[i] < cmk[bi])) bi = i;
-        uint32_t k = ncand;
+        uint32_t k = ncand;  // <= 3 + 14 + 64, so the 16 heads stay below kSpec0
         if (bi < kMaxCand && cmk[bi] < __builtin_inff()) {
-            const uint32_t hb = chead[bi], fb = cf[bi];
+            const uint32_t h2 = chead[bi], f2 = cf[bi];
+            auto head = [&](uint32_t h) {
+                put(k, 0, h, f2);
+                const uint32_t e = h < hb ? hb - h : h - hb;  // its spec slot, if any
+                if (f2 == fb && h == hb) {
+                    cmk[k] = cmk[0];
+                } else if (f2 == fb && e >= 1u && e <= kSpec / 2u && sval[2u * (e - 1u) + (h > hb ? 1u : 0u)]) {
+                    cmk[k] = cmk[kSpec0 + 2u * (e - 1u) + (h > hb ? 1u : 0u)];
+                } else {
+                    cstate[k] = 2;
+                    ++nmiss;
+                }
+                ++k;
+            };
             for (uint32_t d = 1; d <= 8; ++d) {  // the grid steps ~16 heads
-                if (hb >= d && k < kMaxCand) {
-                    cmode[k] = 0;
-                    chead[k] = hb - d;
-                    cf[k++] = fb;
-                }
-                if (hb + d <= hcap && hb + d < G && k < kMaxCand) {
-                    cmode[k] = 0;
-                    chead[k] = hb + d;
-                    cf[k++] = fb;
-                }
+                if (h2 >= d && k < kSpec0) head(h2 - d);
+                if (h2 + d <= hcap && h2 + d < G && k < kSpec0) head(h2 + d);
             }
         }
         nref = k;
     }
     __syncthreads();
-    {
-        const bool run = c >= ncand && c < nref;
+    if (nmiss) {
+        const bool run = c >= ncand && c < nref && cstate[c] == 2;
         float mk = __builtin_inff();
-        if (run) mk = sim_xcd(blocks, L, G, cmode[c], chead[c], cf[c], x, cus / kSimXcds);
+        if (run) mk = sim_xcd(blocks, L, G, cmode[c], chead[c], cf[c], x, xcus);
 #pragma unroll
         for (uint32_t m = 1; m < kSimXcds; m *= 2) mk = fmaxf(mk, __shfl_xor(mk, m));
         if (x == 0 && run) cmk[c] = mk;
         __syncthreads();
-        if (t == 0) ts[5] = __builtin_amdgcn_s_memrealtime();
     }
     if (t == 0) {
+        ts[5] = __builtin_amdgcn_s_memrealtime();
+        cs[5] = __builtin_amdgcn_s_memtime();
         uint32_t bi = 0;
         for (uint32_t i = 1; i < nref; ++i)
             if (cmk[i] < cmk[bi]) bi = i;
@@ -794,6 +883,8 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         plan[2] = cmode[bi] == 1 ? 0u : cf[bi];
 #pragma unroll
         for (int i = 1; i < 6; ++i) plan[7 + i] = static_cast<uint32_t>(ts[i] - ts[0]);
+#pragma unroll
+        for (int i = 1; i < 6; ++i) plan[13 + i] = static_cast<uint32_t>(cs[i] - cs[0]);
     }
 }
 

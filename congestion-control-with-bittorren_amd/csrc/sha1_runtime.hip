@@ -370,14 +370,17 @@ int launch_mixed_checked(const BatchArgs& A, const uint32_t* sorted_len, uint32_
     hipError_t e = launch_mixed(A, sorted_len, plan, cus, force ? forced : nullptr, st);
     if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "mixed kernel launch: %s", hipGetErrorString(e));
     if (const char* d = getenv("SHA1CHUNK_MIXED_DEBUG"); d && atoi(d)) {
-        uint32_t p[14];
+        uint32_t p[19];
         HIP_TRY(hipMemcpyAsync(p, plan, sizeof p, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         fprintf(stderr, "sha1chunk mixed plan: n=%u groups=%u cus=%d mode=%u H=%u F=%u\n", A.n,
                 (A.n + 63u) / 64u, cus, p[0], p[1], p[2]);
         if (!force && p[12])  // the planner's stage end times (us since its start)
-            fprintf(stderr, "sha1chunk mixed planner stages: scan %.1f bounds %.1f sim1 %.1f sim2 %.1f sim3 %.1f us\n",
-                    p[8] * 0.01, p[9] * 0.01, p[10] * 0.01, p[11] * 0.01, p[12] * 0.01);
+            fprintf(stderr,
+                    "sha1chunk mixed planner stages: scan %.1f bounds %.1f sim1 %.1f sim2 %.1f sim3 %.1f us;"
+                    " kcycles %.1f %.1f %.1f %.1f %.1f\n",
+                    p[8] * 0.01, p[9] * 0.01, p[10] * 0.01, p[11] * 0.01, p[12] * 0.01, p[14] * 1e-3, p[15] * 1e-3,
+                    p[16] * 1e-3, p[17] * 1e-3, p[18] * 1e-3);
     }
     return SHA1CHUNK_OK;
 }

@@ -13,15 +13,17 @@
 // prices such a group by its first chunk, the hashing is unaffected).
 //
 // Up to kSortMaxTiles tiles of 4096 chunks (1 Mi chunks) an LSD radix sort
-// of two 8-bit digits in three launches of its own:
-//   sort_keys_hist   keys, and each tile's low-digit histogram
-//   sort_scatter<1>  stable scatter by the low digit; the high-digit
-//                    histograms of the tiles it writes into (atomics)
+// of two 8-bit digits in four launches of its own:
+//   sort_hist<1>     keys, and each tile's low-digit histogram
+//   sort_scatter<1>  stable scatter by the low digit
+//   sort_hist<2>     each tile's high-digit histogram of that order (its
+//                    own launch: global atomics from the scatter serialised,
+//                    40 against 24 us at 131072 chunks in arrival order)
 //   sort_scatter<2>  stable scatter by the high digit: the order, and the
 //                    sorted lengths the planner reads
 // A tile's start for digit d is the count of d in the tiles before it plus
 // every larger digit's total, each workgroup summing the histogram columns
-// itself (T loads per thread), so no scan launch.  Inside a tile, rank =
+// itself (T / 4 loads per thread), so no scan launch.  Inside a tile, rank =
 // (earlier (item, wave) slices' count of d) + (lanes of the wave below this
 // one with the same digit, from 8 ballots).  rocPRIM's radix sort took
 // ~51 us at 131072 chunks (a block sort and seven merge passes on 32-bit
@@ -40,8 +42,13 @@
 namespace {
 inline size_t align256(size_t x) { return (x + 255) & ~size_t(255); }
 
-constexpr uint32_t kSortThreads = 256, kSortItems = 16, kSortWaves = kSortThreads / 64;
+// A tile of 4096 chunks per workgroup of 16 waves, 4 chunks per lane
+// (chunk base + item * 1024 + thread): 16 waves keep each lane's chains of
+// dependent loads and LDS steps short (4 waves of 16 items each: 21-40 us
+// per scatter at 131072 chunks, profiles/fixed_cost_r05.log).
+constexpr uint32_t kSortThreads = 1024, kSortItems = 4, kSortWaves = kSortThreads / 64;
 constexpr uint32_t kSortTile = kSortThreads * kSortItems;  // 4096 chunks
+constexpr uint32_t kSortSlices = kSortItems * kSortWaves;  // (item, wave) slices of a tile, in chunk order
 constexpr uint32_t kSortMaxTiles = 256;
 
 __device__ __forceinline__ uint16_t block_key(uint32_t len) {
@@ -54,83 +61,116 @@ template <int PASS>
 __device__ __forceinline__ uint32_t key_slot(uint32_t k) {
     return 255u - (PASS == 1 ? (k & 255u) : (k >> 8));
 }
+
+// The valid lanes of the wave whose slot equals this lane's (8 ballots).
+__device__ __forceinline__ uint64_t slot_peers(bool valid, uint32_t s) {
+    uint64_t m = __ballot(valid);
+#pragma unroll
+    for (uint32_t b = 0; b < 8u; ++b) {
+        const uint64_t bal = __ballot((s >> b) & 1u);
+        m &= ((s >> b) & 1u) ? bal : ~bal;
+    }
+    return m;
+}
+
+__device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
 }  // namespace
 
-// Tile t: keys[i] for its chunks, hist1[t][slot] of their low digits, and
-// hist2[t][*] zeroed for sort_scatter<1>'s atomics.
-__global__ __launch_bounds__(kSortThreads) void sort_keys_hist(const uint32_t* len, uint16_t* keys, uint32_t* hist1,
-                                                               uint32_t* hist2, uint32_t n) {
+// Tile blockIdx.x's slot histogram of digit PASS: PASS 1 from the lengths
+// (writing the keys), PASS 2 from the first scatter's keys.  One LDS atomic
+// per run of equal slots in a wave (a tile of equal keys otherwise
+// serialises 4096 atomics on one bin).
+template <int PASS>
+__global__ __launch_bounds__(kSortThreads) void sort_hist(const uint32_t* len, const uint16_t* keys_in,
+                                                          uint16_t* keys_out, uint32_t* hist, uint32_t n) {
     __shared__ uint32_t h[256];
     const uint32_t tid = threadIdx.x;
-    h[tid] = 0u;
+    if (tid < 256u) h[tid] = 0u;
     __syncthreads();
     const uint32_t base = blockIdx.x * kSortTile;
 #pragma unroll
     for (uint32_t it = 0; it < kSortItems; ++it) {
         const uint32_t i = base + it * kSortThreads + tid;
-        if (i < n) {
-            const uint16_t k = block_key(len[i]);
-            keys[i] = k;
-            atomicAdd(&h[key_slot<1>(k)], 1u);
+        const bool valid = i < n;
+        uint32_t k = 0;
+        if (valid) {
+            if constexpr (PASS == 1) {
+                k = block_key(len[i]);
+                keys_out[i] = (uint16_t)k;
+            } else {
+                k = keys_in[i];
+            }
         }
+        const uint32_t s = key_slot<PASS>(k);
+        const uint64_t m = slot_peers(valid, s);
+        if (valid && lanes_below(m) == 0u) atomicAdd(&h[s], (uint32_t)__popcll(m));
     }
     __syncthreads();
-    hist1[blockIdx.x * 256u + tid] = h[tid];
-    hist2[blockIdx.x * 256u + tid] = 0u;
+    if (tid < 256u) hist[blockIdx.x * 256u + tid] = h[tid];
 }
 
-// One stable counting-sort pass over 8-bit digit PASS of tile blockIdx.x's
-// keys (keys_in / ids_in in the previous pass's order; ids_in null = the
-// chunk index).  PASS 1 writes keys_out / ids_out and counts the high digit
-// of what lands in each output tile into hist_next; PASS 2 writes the final
-// order and sorted lengths.
+// One stable counting-sort pass over digit PASS of tile blockIdx.x (keys_in
+// / ids_in in the previous pass's order; ids_in null = the chunk index):
+// PASS 1 writes keys_out / ids_out, PASS 2 the order and sorted lengths.
 template <int PASS>
 __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint16_t* keys_in, const uint32_t* ids_in,
                                                              const uint32_t* hist, uint32_t tiles, uint32_t n,
                                                              uint16_t* keys_out, uint32_t* ids_out,
-                                                             uint32_t* hist_next, const uint32_t* len,
-                                                             uint32_t* sorted_len) {
-    __shared__ uint32_t start[256];                         // the tile's first position per slot
-    __shared__ uint32_t scan[256];
-    __shared__ uint16_t cnt[kSortItems * kSortWaves][256];  // per (item, wave) slice, then its prefix
-    const uint32_t tid = threadIdx.x, wave = tid >> 6;
+                                                             const uint32_t* len, uint32_t* sorted_len) {
+    __shared__ uint32_t start[256];                   // the tile's first position per slot
+    __shared__ uint32_t part_tot[4][256], part_pre[4][256], wsum[4];
+    __shared__ uint16_t cnt[kSortSlices][256];        // per (item, wave) slice, then its prefix
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
     const uint32_t tile = blockIdx.x;
 
-    // this slot's count over all tiles and over the tiles before this one
-    uint32_t tot = 0, pre = 0;
+    // slot s = tid % 256 over a quarter q = tid / 256 of the tiles: its
+    // count in all of them and in those before this one
     {
-        uint32_t t = 0;
-        for (; t + 8u <= tiles; t += 8u) {
+        const uint32_t s = tid & 255u, q = tid >> 8, per = (tiles + 3u) / 4u;
+        const uint32_t t0 = min(tiles, q * per), t1 = min(tiles, t0 + per);
+        uint32_t tot = 0, pre = 0, t = t0;
+        for (; t + 8u <= t1; t += 8u) {
             uint32_t v[8];
 #pragma unroll
-            for (uint32_t u = 0; u < 8u; ++u) v[u] = hist[(t + u) * 256u + tid];
+            for (uint32_t u = 0; u < 8u; ++u) v[u] = hist[(t + u) * 256u + s];
 #pragma unroll
             for (uint32_t u = 0; u < 8u; ++u) {
                 tot += v[u];
                 pre += t + u < tile ? v[u] : 0u;
             }
         }
-        for (; t < tiles; ++t) {
-            const uint32_t v = hist[t * 256u + tid];
+        for (; t < t1; ++t) {
+            const uint32_t v = hist[t * 256u + s];
             tot += v;
             pre += t < tile ? v : 0u;
         }
-    }
-    // exclusive scan of the slot totals (inclusive Hillis-Steele, minus own)
-    scan[tid] = tot;
-    __syncthreads();
-    for (uint32_t off = 1; off < 256u; off <<= 1) {
-        const uint32_t v = tid >= off ? scan[tid - off] : 0u;
-        __syncthreads();
-        scan[tid] += v;
-        __syncthreads();
-    }
-    start[tid] = scan[tid] - tot + pre;
-    {
+        part_tot[q][s] = tot;
+        part_pre[q][s] = pre;
         uint32_t* c32 = reinterpret_cast<uint32_t*>(&cnt[0][0]);
-        for (uint32_t w = tid; w < kSortItems * kSortWaves * 128u; w += kSortThreads) c32[w] = 0u;
+        for (uint32_t w = tid; w < kSortSlices * 128u; w += kSortThreads) c32[w] = 0u;
     }
     __syncthreads();
+    // slots' exclusive scan of their totals (waves 0-3, a slot per lane)
+    if (tid < 256u) {
+        const uint32_t tot = part_tot[0][tid] + part_tot[1][tid] + part_tot[2][tid] + part_tot[3][tid];
+        const uint32_t pre = part_pre[0][tid] + part_pre[1][tid] + part_pre[2][tid] + part_pre[3][tid];
+        uint32_t inc = tot;
+#pragma unroll
+        for (uint32_t d = 1; d < 64u; d <<= 1) {
+            const uint32_t v = __shfl_up(inc, d);
+            if (lane >= d) inc += v;
+        }
+        if (lane == 63u) wsum[wave] = inc;
+        part_tot[0][tid] = inc - tot + pre;  // exclusive within the wave, plus earlier tiles
+    }
+    __syncthreads();
+    if (tid < 256u) {
+        uint32_t off = 0;
+        for (uint32_t w = 0; w < wave; ++w) off += wsum[w];
+        start[tid] = part_tot[0][tid] + off;
+    }
 
     // rank inside the wave: valid lanes below this one with the same slot
     const uint32_t base = tile * kSortTile;
@@ -143,25 +183,30 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint16_t* key
         const uint32_t k = valid ? keys_in[i] : 0u;
         id[it] = valid ? (ids_in ? ids_in[i] : i) : 0u;
         const uint32_t s = key_slot<PASS>(k);
-        uint64_t m = __ballot(valid);
-#pragma unroll
-        for (uint32_t b = 0; b < 8u; ++b) {
-            const uint64_t bal = __ballot((s >> b) & 1u);
-            m &= ((s >> b) & 1u) ? bal : ~bal;
-        }
-        const uint32_t below =
-            __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const uint64_t m = slot_peers(valid, s);
+        const uint32_t below = lanes_below(m);
         if (valid && below == 0u) cnt[it * kSortWaves + wave][s] = (uint16_t)__popcll(m);
         key_rank[it] = k | (below << 16);
     }
     __syncthreads();
-    // per slot: the slices' exclusive prefix inside the tile, in (item, wave) order
+    // per slot: the slices' exclusive prefix inside the tile, in (item, wave)
+    // order; thread (q, s) takes slices 16q .. 16q+15
     {
+        const uint32_t s = tid & 255u, q = tid >> 8;
+        uint32_t c[16], sum = 0;
+#pragma unroll
+        for (uint32_t u = 0; u < 16u; ++u) {
+            c[u] = cnt[16u * q + u][s];
+            sum += c[u];
+        }
+        part_pre[q][s] = sum;
+        __syncthreads();
         uint32_t run = 0;
-        for (uint32_t q = 0; q < kSortItems * kSortWaves; ++q) {
-            const uint32_t c = cnt[q][tid];
-            cnt[q][tid] = (uint16_t)run;
-            run += c;
+        for (uint32_t w = 0; w < q; ++w) run += part_pre[w][s];
+#pragma unroll
+        for (uint32_t u = 0; u < 16u; ++u) {
+            cnt[16u * q + u][s] = (uint16_t)run;
+            run += c[u];
         }
     }
     __syncthreads();
@@ -175,7 +220,6 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint16_t* key
             if constexpr (PASS == 1) {
                 keys_out[dst] = (uint16_t)k;
                 ids_out[dst] = id[it];
-                atomicAdd(&hist_next[(dst / kSortTile) * 256u + key_slot<2>(k)], 1u);
             } else {
                 ids_out[dst] = id[it];
                 sorted_len[dst] = len[id[it]];
@@ -234,11 +278,14 @@ hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t
         uint32_t* hist1 = reinterpret_cast<uint32_t*>(temp);
         uint32_t* hist2 = reinterpret_cast<uint32_t*>(temp + hb);
         uint32_t* ids2 = reinterpret_cast<uint32_t*>(temp + 2 * hb);
-        hipLaunchKernelGGL(sort_keys_hist, dim3(tiles), dim3(kSortThreads), 0, st, d_len, keys, hist1, hist2, n);
+        hipLaunchKernelGGL(sort_hist<1>, dim3(tiles), dim3(kSortThreads), 0, st, d_len, (const uint16_t*)nullptr,
+                           keys, hist1, n);
         hipLaunchKernelGGL(sort_scatter<1>, dim3(tiles), dim3(kSortThreads), 0, st, keys, (const uint32_t*)nullptr,
-                           hist1, tiles, n, keys2, ids2, hist2, (const uint32_t*)nullptr, (uint32_t*)nullptr);
+                           hist1, tiles, n, keys2, ids2, (const uint32_t*)nullptr, (uint32_t*)nullptr);
+        hipLaunchKernelGGL(sort_hist<2>, dim3(tiles), dim3(kSortThreads), 0, st, (const uint32_t*)nullptr, keys2,
+                           (uint16_t*)nullptr, hist2, n);
         hipLaunchKernelGGL(sort_scatter<2>, dim3(tiles), dim3(kSortThreads), 0, st, keys2, ids2, hist2, tiles, n,
-                           (uint16_t*)nullptr, order, (uint32_t*)nullptr, d_len, sorted_len);
+                           (uint16_t*)nullptr, order, d_len, sorted_len);
         e = hipGetLastError();
     } else {
         const dim3 grid((n + 255u) / 256u);

@@ -64,6 +64,8 @@ def main():
     ap.add_argument("--misalign", action="store_true",
                     help="hash each chunk from 1..15 bytes past its (16-byte aligned) start, 16 bytes "
                          "shorter: no wave has all lanes 16-byte aligned (the per-lane load path)")
+    ap.add_argument("--b2b", type=int, default=0,
+                    help="after the timed calls, K more enqueued back to back (one sync): ms per call")
     ap.add_argument("--out", default=None)
     ap.add_argument("--lib", default=None, help="A/B: load this libsha1chunk.so (and its backend) instead")
     a = ap.parse_args()
@@ -138,6 +140,14 @@ def main():
                     torch.cuda.synchronize()
                     if r:
                         ts.append(time.perf_counter() - t0)
+                b2b = None
+                if a.b2b:  # K calls enqueued back to back, one sync: the chip stays busy
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    for _ in range(a.b2b):
+                        pkg.hash_device(base, d_off, d_len, dig, kernel=kernel)
+                    torch.cuda.synchronize()
+                    b2b = round((time.perf_counter() - t0) / a.b2b * 1e3, 3)
             finally:
                 for k, v in old.items():
                     if v is None:
@@ -158,6 +168,8 @@ def main():
                    "uniform": a.uniform, "payload_bytes": nbytes, "ms": round(sec * 1e3, 3),
                    "payload_GiBps": round(nbytes / sec / 2**30, 2), "runs_ms": [round(t * 1e3, 3) for t in ts],
                    "longest_blocks": int(lens.max()) // 64 + 2, "parity": ok}
+            if b2b is not None:
+                row["back_to_back_ms_per_call"] = b2b
             print(json.dumps(row), flush=True)
             rows.append(row)
         del base
