@@ -609,8 +609,8 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         return;
     }
     __shared__ uint64_t scan[kPlanThreads];
-    __shared__ double best_m[kPlanThreads];
-    __shared__ uint32_t best_h[kPlanThreads], best_f[kPlanThreads];
+    __shared__ double best_m[kPlanThreads / 64];
+    __shared__ uint32_t best_h[kPlanThreads / 64], best_f[kPlanThreads / 64];
     __shared__ uint64_t prefix[kPlanMaxH + 1];
     const uint32_t G = (n + 63u) / 64u;
     const uint32_t per = (G + kPlanThreads - 1) / kPlanThreads;
@@ -630,17 +630,27 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         if (w < kSimMaxG / 32) togw[w] = lay_bits[w];
         local_t += lay_tb[w];
     }
-    __syncthreads();
-    scan[t] = local;
-    atomicAdd(reinterpret_cast<unsigned long long*>(&tog_blocks), static_cast<unsigned long long>(local_t));
-    __syncthreads();
-    for (uint32_t off = 1; off < kPlanThreads; off <<= 1) {
-        const uint64_t v = t >= off ? scan[t - off] : 0ull;
-        __syncthreads();
-        scan[t] += v;
-        __syncthreads();
+    // inclusive scan of the threads' block counts: in the wave, then over
+    // the 16 wave totals (Hillis-Steele over the workgroup took 20 barriers)
+    const uint32_t lane = t & 63u, wv = t >> 6;
+    __shared__ uint64_t wtot[kPlanThreads / 64];
+    uint64_t inc = local;
+#pragma unroll
+    for (uint32_t d = 1; d < 64u; d <<= 1) {
+        const uint64_t v = __shfl_up(inc, d);
+        if (lane >= d) inc += v;
     }
-    const uint64_t PG = scan[kPlanThreads - 1];
+    for (uint32_t m = 32; m >= 1; m >>= 1) local_t += __shfl_xor(local_t, m);
+    if (lane == 63u) wtot[wv] = inc;
+    if (lane == 0u) atomicAdd(reinterpret_cast<unsigned long long*>(&tog_blocks), static_cast<unsigned long long>(local_t));
+    __syncthreads();
+    uint64_t before = 0, PG = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kPlanThreads / 64; ++w) {
+        before += w < wv ? wtot[w] : 0ull;
+        PG += wtot[w];
+    }
+    scan[t] = before + inc;
     const double ft = PG ? (double)tog_blocks / (double)PG : 1.0;
     if (t == 0) {
         ts[1] = __builtin_amdgcn_s_memrealtime();
@@ -657,6 +667,8 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     }
     __syncthreads();
     const PlanLayout L{run8, ft >= 0.5};
+    uint64_t bsub[3] = {0, 0, 0};  // shader-clock stamps inside the bounds stage (plan[24..26])
+    if (t == 0) bsub[0] = __builtin_amdgcn_s_memtime();
     // P_H for every candidate H <= hcap, then each thread takes H = t, t + 1024, ..
     uint64_t P = scan[t] - local;  // P_{g0}
     for (uint32_t g = g0; g <= g1 && g <= hcap; ++g) {
@@ -664,34 +676,62 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         if (g < g1) P += plan_blocks(sorted_len, blocks, g);
     }
     __syncthreads();
+    if (t == 0) bsub[1] = __builtin_amdgcn_s_memtime();
+    // every (H, F): H in [0, hcap] with F = 4 and, below G, 8, and H = G
+    // (every group split) beyond hcap; pair w = 2H + (F == 8), the last one
+    // H = G, dealt evenly over the threads (thread 0 took H = 0, 1024 and G
+    // at 2048 groups: 5 bounds against 2)
     double bm = 1e300;
     uint32_t bh = 0, bf = 4;
-    for (uint32_t H = t; H <= hcap; H += kPlanThreads) {
-        for (uint32_t F = 4; F <= (H < G ? 8u : 4u); F += 4) {  // H = G: every group split
-            const double m = makespan(sorted_len, blocks, L, ft, G, cus, 0, H, F, prefix[H], PG);
-            if (m < bm) { bm = m; bh = H; bf = F; }
+    const uint32_t npair = 2u * (hcap + 1u) + (G > hcap ? 1u : 0u);
+    for (uint32_t w = t; w < npair; w += kPlanThreads) {
+        const bool all = w == 2u * (hcap + 1u);  // H = G beyond hcap
+        const uint32_t H = all ? G : w / 2u, F = all ? 4u : 4u + 4u * (w & 1u);
+        if (F == 8u && H >= G) continue;  // H = G: every group split, F = 4 only
+        const double m = makespan(sorted_len, blocks, L, ft, G, cus, 0, H, F, all ? PG : prefix[H], PG);
+        if (m < bm || (m == bm && (H < bh || (H == bh && F < bf)))) { bm = m; bh = H; bf = F; }
+    }
+    if (t == 0) bsub[2] = __builtin_amdgcn_s_memtime();
+    // the smallest (bound, head, F) over the workgroup: in the wave, then
+    // over the 16 waves' bests
+#pragma unroll
+    for (uint32_t m = 32; m >= 1; m >>= 1) {
+        const double mo = __shfl_xor(bm, m);
+        const uint32_t ho = __shfl_xor(bh, m), fo = __shfl_xor(bf, m);
+        if (mo < bm || (mo == bm && (ho < bh || (ho == bh && fo < bf)))) {
+            bm = mo;
+            bh = ho;
+            bf = fo;
         }
     }
-    if (t == 0 && G > hcap) {  // H = G beyond the searched head sizes
-        const double m = makespan(sorted_len, blocks, L, ft, G, cus, 0, G, 4, PG, PG);
-        if (m < bm) { bm = m; bh = G; bf = 4; }
+    if (lane == 0u) {
+        best_m[wv] = bm;
+        best_h[wv] = bh;
+        best_f[wv] = bf;
     }
-    best_m[t] = bm;
-    best_h[t] = bh;
-    best_f[t] = bf;
     __syncthreads();
-    for (uint32_t s = kPlanThreads / 2; s > 0; s >>= 1) {
-        if (t < s) {
-            const double mo = best_m[t + s];
-            const uint32_t ho = best_h[t + s];
-            if (mo < best_m[t] || (mo == best_m[t] && ho < best_h[t])) {
-                best_m[t] = mo;
-                best_h[t] = ho;
-                best_f[t] = best_f[t + s];
+    if (t < 64) {  // the 16 waves' bests, reduced by wave 0
+        constexpr uint32_t kW = kPlanThreads / 64;
+        bm = t < kW ? best_m[t] : 1e300;
+        bh = t < kW ? best_h[t] : 0xffffffffu;
+        bf = t < kW ? best_f[t] : 8u;
+#pragma unroll
+        for (uint32_t m = kW / 2; m >= 1; m >>= 1) {
+            const double mo = __shfl_xor(bm, m);
+            const uint32_t ho = __shfl_xor(bh, m), fo = __shfl_xor(bf, m);
+            if (mo < bm || (mo == bm && (ho < bh || (ho == bh && fo < bf)))) {
+                bm = mo;
+                bh = ho;
+                bf = fo;
             }
         }
-        __syncthreads();
+        if (t == 0) {
+            best_m[0] = bm;
+            best_h[0] = bh;
+            best_f[0] = bf;
+        }
     }
+    __syncthreads();
     if (t == 0) {
         ts[2] = __builtin_amdgcn_s_memrealtime();
         cs[2] = __builtin_amdgcn_s_memtime();
@@ -717,11 +757,12 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     // below G, 8.  Wave 0 builds the list in parallel (positions from
     // ballots), then each candidate's makespan bounds are computed once.
     constexpr uint32_t kMaxCand = kPlanThreads / kSimXcds;
-    constexpr uint32_t kSpec = 16, kSpec0 = kMaxCand - kSpec;  // heads hb -/+ 1..8 simulated ahead
-    __shared__ uint32_t cmode[kMaxCand], chead[kMaxCand], cf[kMaxCand], ncand, nref, npend, nmiss;
-    __shared__ float cmk[kMaxCand];
+    constexpr uint32_t kSpec = 32;  // heads hb -/+ 1..16, simulated in the first sweep
+    __shared__ uint32_t cmode[kMaxCand], chead[kMaxCand], cf[kMaxCand], ncand, nref, npend, nmiss, nrun;
+    __shared__ float cmk[kMaxCand], scmk[kSpec];
     __shared__ double clb[kMaxCand];
     __shared__ uint8_t cstate[kMaxCand], sval[kSpec];
+    __shared__ uint8_t runidx[kMaxCand];  // the first sweep's work: slot, or 128 + early head
     const uint32_t hb = best_h[0], fb = best_f[0];
     const double mb = best_m[0];
     auto put = [&](uint32_t k, uint32_t m, uint32_t h, uint32_t f) {
@@ -763,15 +804,41 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         const uint32_t q = t - 64u, d = q / 2u + 1u;
         const bool ok = hb < G && ((q & 1u) == 0u ? hb >= d : (hb + d <= hcap && hb + d < G));
         sval[q] = ok ? 1 : 0;
-        put(kSpec0 + q, 0, (q & 1u) == 0u ? hb - d : hb + d, fb);
     }
     __syncthreads();
+    uint64_t sub[3] = {0, 0, 0};  // shader-clock stamps inside the first sweep's stage (plan[20..22])
+    if (t == 0) sub[0] = __builtin_amdgcn_s_memtime();
     if (t >= 1 && t < ncand) {
         const uint32_t m = cmode[t], h = chead[t], f = cf[t];
         clb[t] = m == 1 ? makespan(sorted_len, blocks, L, ft, G, cus, 1, 0, 0, 0, PG)
                         : makespan(sorted_len, blocks, L, ft, G, cus, 0, h, f, h <= hcap ? prefix[h] : PG, PG);
     }
     __syncthreads();
+    if (t == 0) sub[1] = __builtin_amdgcn_s_memtime();
+    // the first sweep's work, packed onto the fewest waves (8 lanes each):
+    // the bounds' plan, candidates within 5 % of its bounds, early heads
+    // (and no longer chain than 1.25x its: a sweep lasts as long as its
+    // longest candidate, and all-split's 2048 jobs at 2048 groups, often
+    // within 5 % by its bounds, tripled it)
+    const double early = mb * 1.05;
+    const uint32_t jcap = plan_jobs(G, 0, hb, fb) + plan_jobs(G, 0, hb, fb) / 4u;
+    if (t < 64) {
+        uint32_t off = 0;
+        for (uint32_t i = t; i < kMaxCand + kSpec; i += 64) {
+            const bool w = i < kMaxCand ? (i == 0 || (i < ncand && clb[i] < early &&
+                                                      plan_jobs(G, cmode[i], chead[i], cf[i]) <= jcap))
+                                        : sval[i - kMaxCand] != 0;
+            const uint64_t bal = __ballot(w);
+            if (w) {
+                runidx[off + __popcll(bal & ((1ull << t) - 1ull))] = static_cast<uint8_t>(i);
+                if (i < kMaxCand) cstate[i] = 3;  // simulated in the first sweep
+            }
+            off += __popcll(bal);
+        }
+        if (t == 0) nrun = off;  // <= 1 + 80 + 32 (kMaxCand + kSpec slots: 160 fit the uint8 indices)
+    }
+    __syncthreads();
+    if (t == 0) sub[2] = __builtin_amdgcn_s_memtime();
     // Pass 1 simulates the bounds' plan; pass 2 every other candidate whose
     // bounds are below that time (the rest cannot beat it; a 4096-group
     // all-split candidate alone is ~100 us of simulation); pass 3 the heads
@@ -784,14 +851,23 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     // chain of inserts, so this is one sweep instead of three in the usual
     // case.  The choice is the same as passes 1-3 in order.
     const uint32_t c = t / kSimXcds, x = t % kSimXcds, xcus = cus / kSimXcds;
-    const double early = mb * 1.05;
     {
-        const bool run = c == 0 || (c < ncand && clb[c] < early) || (c >= kSpec0 && sval[c - kSpec0]);
+        const bool run = c < nrun;
+        const uint32_t i = run ? runidx[c] : 0u, q = i - kMaxCand, d = q / 2u + 1u;
+        const bool main = i < kMaxCand;
+        // one call: two (one per kind of work) ran one after the other in a wave holding both
+        const uint32_t sm = main ? cmode[i] : 0u, sh = main ? chead[i] : ((q & 1u) == 0u ? hb - d : hb + d);
+        const uint32_t sf = main ? cf[i] : fb;
         float mk = __builtin_inff();
-        if (run) mk = sim_xcd(blocks, L, G, cmode[c], chead[c], cf[c], x, xcus);
+        if (run) mk = sim_xcd(blocks, L, G, sm, sh, sf, x, xcus);
 #pragma unroll
         for (uint32_t m = 1; m < kSimXcds; m *= 2) mk = fmaxf(mk, __shfl_xor(mk, m));
-        if (x == 0 && run) cmk[c] = mk;
+        if (x == 0 && run) {
+            if (main)
+                cmk[i] = mk;
+            else
+                scmk[q] = mk;
+        }
         __syncthreads();
         if (t == 0) {
             ts[3] = __builtin_amdgcn_s_memrealtime();
@@ -803,7 +879,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     if (t >= 1 && t < ncand) {
         if (!(clb[t] < (double)cmk[0])) {
             cmk[t] = __builtin_inff();
-        } else if (!(clb[t] < early)) {
+        } else if (cstate[t] != 3) {
             cstate[t] = 1;
             atomicAdd(&npend, 1u);
         }
@@ -830,32 +906,48 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     // 14.09 / 14.27, H = 176 14.35 / 14.41) and the grid above steps ~16
     // heads, so every head within 8 of the best split-head plan is tried
     // (taken from the first sweep when it simulated that head).
-    if (t == 0) {
-        uint32_t bi = kMaxCand;  // the shortest mode-0 candidate with a fused tail
-        for (uint32_t i = 0; i < ncand; ++i)
-            if (cmode[i] == 0 && chead[i] < G && (bi == kMaxCand || cmk[i] < cmk[bi])) bi = i;
-        uint32_t k = ncand;  // <= 3 + 14 + 64, so the 16 heads stay below kSpec0
-        if (bi < kMaxCand && cmk[bi] < __builtin_inff()) {
-            const uint32_t h2 = chead[bi], f2 = cf[bi];
-            auto head = [&](uint32_t h) {
-                put(k, 0, h, f2);
-                const uint32_t e = h < hb ? hb - h : h - hb;  // its spec slot, if any
-                if (f2 == fb && h == hb) {
-                    cmk[k] = cmk[0];
-                } else if (f2 == fb && e >= 1u && e <= kSpec / 2u && sval[2u * (e - 1u) + (h > hb ? 1u : 0u)]) {
-                    cmk[k] = cmk[kSpec0 + 2u * (e - 1u) + (h > hb ? 1u : 0u)];
-                } else {
-                    cstate[k] = 2;
-                    ++nmiss;
-                }
-                ++k;
-            };
-            for (uint32_t d = 1; d <= 8; ++d) {  // the grid steps ~16 heads
-                if (h2 >= d && k < kSpec0) head(h2 - d);
-                if (h2 + d <= hcap && h2 + d < G && k < kSpec0) head(h2 + d);
+    // bi: the shortest mode-0 candidate with a fused tail, first on ties --
+    // the smallest (time bits, index) over the slots (times are >= 0 or
+    // +inf, so their bits order as unsigned integers)
+    __shared__ uint64_t red[kMaxCand / 64];
+    if (t < kMaxCand) {
+        const bool el = t < ncand && cmode[t] == 0 && chead[t] < G;
+        uint64_t key = el ? (uint64_t)__float_as_uint(cmk[t]) << 32 | t : ~0ull;
+#pragma unroll
+        for (uint32_t m = 32; m >= 1; m >>= 1) key = min(key, (uint64_t)__shfl_xor(key, m));
+        if (lane == 0u) red[wv] = key;
+    }
+    __syncthreads();
+    if (t < 64) {  // the 16 heads, lane j: d = j / 2 + 1, below (j even) or above bi's head
+        uint64_t key = red[0];
+#pragma unroll
+        for (uint32_t w = 1; w < kMaxCand / 64; ++w) key = min(key, red[w]);
+        const bool have = (uint32_t)(key >> 32) < 0x7f800000u;  // some candidate, and finite
+        const uint32_t bi = (uint32_t)key;
+        const uint32_t h2 = have ? chead[bi] : 0u, f2 = have ? cf[bi] : 4u, d = t / 2u + 1u;
+        const bool lo = (t & 1u) == 0u;
+        const bool ok = have && t < 16u && (lo ? h2 >= d : (h2 + d <= hcap && h2 + d < G));
+        const uint32_t h = lo ? h2 - d : h2 + d;
+        const uint32_t k = ncand + __popcll(__ballot(ok) & ((1ull << t) - 1ull));  // < kMaxCand: ncand <= 81
+        bool miss = false;
+        if (ok) {
+            put(k, 0, h, f2);
+            const uint32_t e = h < hb ? hb - h : h - hb;  // its early slot, if any
+            const uint32_t q = e >= 1u ? 2u * (e - 1u) + (h > hb ? 1u : 0u) : 0u;
+            if (f2 == fb && h == hb) {
+                cmk[k] = cmk[0];
+            } else if (f2 == fb && e >= 1u && e <= kSpec / 2u && sval[q]) {
+                cmk[k] = scmk[q];
+            } else {
+                cstate[k] = 2;
+                miss = true;
             }
         }
-        nref = k;
+        const uint64_t ballot_ok = __ballot(ok), ballot_miss = __ballot(miss);
+        if (t == 0) {
+            nref = ncand + __popcll(ballot_ok);
+            nmiss = __popcll(ballot_miss);
+        }
     }
     __syncthreads();
     if (nmiss) {
@@ -867,12 +959,21 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         if (x == 0 && run) cmk[c] = mk;
         __syncthreads();
     }
+    // the shortest of all, first on ties
+    if (t < kMaxCand) {
+        uint64_t key = t < nref ? (uint64_t)__float_as_uint(cmk[t]) << 32 | t : ~0ull;
+#pragma unroll
+        for (uint32_t m = 32; m >= 1; m >>= 1) key = min(key, (uint64_t)__shfl_xor(key, m));
+        if (lane == 0u) red[wv] = key;
+    }
+    __syncthreads();
     if (t == 0) {
         ts[5] = __builtin_amdgcn_s_memrealtime();
         cs[5] = __builtin_amdgcn_s_memtime();
-        uint32_t bi = 0;
-        for (uint32_t i = 1; i < nref; ++i)
-            if (cmk[i] < cmk[bi]) bi = i;
+        uint64_t key = red[0];
+#pragma unroll
+        for (uint32_t w = 1; w < kMaxCand / 64; ++w) key = min(key, red[w]);
+        uint32_t bi = (uint32_t)key;
         // All-split (candidate 2) within 0.5 % of the best is taken instead:
         // a chain-bound batch then runs with no fused waves heating the chip
         // (65536 chunks of the config-5 law: 12.14 ms all-split against 12.50
@@ -885,6 +986,11 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         for (int i = 1; i < 6; ++i) plan[7 + i] = static_cast<uint32_t>(ts[i] - ts[0]);
 #pragma unroll
         for (int i = 1; i < 6; ++i) plan[13 + i] = static_cast<uint32_t>(cs[i] - cs[0]);
+#pragma unroll
+        for (int i = 0; i < 3; ++i) plan[20 + i] = static_cast<uint32_t>(sub[i] - cs[0]);
+        plan[23] = nrun;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) plan[24 + i] = static_cast<uint32_t>(bsub[i] - cs[0]);
     }
 }
 

@@ -370,7 +370,7 @@ int launch_mixed_checked(const BatchArgs& A, const uint32_t* sorted_len, uint32_
     hipError_t e = launch_mixed(A, sorted_len, plan, cus, force ? forced : nullptr, st);
     if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "mixed kernel launch: %s", hipGetErrorString(e));
     if (const char* d = getenv("SHA1CHUNK_MIXED_DEBUG"); d && atoi(d)) {
-        uint32_t p[19];
+        uint32_t p[27];
         HIP_TRY(hipMemcpyAsync(p, plan, sizeof p, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         fprintf(stderr, "sha1chunk mixed plan: n=%u groups=%u cus=%d mode=%u H=%u F=%u\n", A.n,
@@ -378,9 +378,11 @@ int launch_mixed_checked(const BatchArgs& A, const uint32_t* sorted_len, uint32_
         if (!force && p[12])  // the planner's stage end times (us since its start)
             fprintf(stderr,
                     "sha1chunk mixed planner stages: scan %.1f bounds %.1f sim1 %.1f sim2 %.1f sim3 %.1f us;"
-                    " kcycles %.1f %.1f %.1f %.1f %.1f\n",
+                    " kcycles %.1f %.1f %.1f %.1f %.1f (bounds: run8 %.1f prefix %.1f search %.1f; first sweep:"
+                    " list %.1f bounds %.1f packed %.1f, %u candidates)\n",
                     p[8] * 0.01, p[9] * 0.01, p[10] * 0.01, p[11] * 0.01, p[12] * 0.01, p[14] * 1e-3, p[15] * 1e-3,
-                    p[16] * 1e-3, p[17] * 1e-3, p[18] * 1e-3);
+                    p[16] * 1e-3, p[17] * 1e-3, p[18] * 1e-3, p[24] * 1e-3, p[25] * 1e-3, p[26] * 1e-3,
+                    p[20] * 1e-3, p[21] * 1e-3, p[22] * 1e-3, p[23]);
     }
     return SHA1CHUNK_OK;
 }

@@ -10,7 +10,7 @@
 #include <vector>
 
 __global__ __launch_bounds__(1024) void sim_probe(const uint32_t* gblocks, const uint8_t* grun, uint32_t G, uint32_t H,
-                                                  uint32_t F, uint64_t* cyc, float* out) {
+                                                  uint32_t F, uint32_t ncand, uint64_t* cyc, float* out) {
     __shared__ uint32_t blocks[kSimMaxG];
     __shared__ uint8_t run8[kSimMaxG];
     for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) {
@@ -22,7 +22,7 @@ __global__ __launch_bounds__(1024) void sim_probe(const uint32_t* gblocks, const
     const uint32_t t = threadIdx.x, c = t / kSimXcds, x = t % kSimXcds;
     const uint64_t c0 = __builtin_amdgcn_s_memtime();
     float mk = 0.0f;
-    if (c == 0) mk = sim_xcd(blocks, L, G, 0, H, F, x, kSimCus);
+    if (c < ncand) mk = sim_xcd(blocks, L, G, 0, H - 8u + c % 17u, F, x, kSimCus);
     const uint64_t c1 = __builtin_amdgcn_s_memtime();
     __syncthreads();
     out[t] = mk;
@@ -46,13 +46,17 @@ int main() {
     (void)hipMemcpy(dr, r.data(), G, hipMemcpyHostToDevice);
     const uint32_t J = H + (G - H + F - 1) / F;
     for (int threads : {64, 1024}) {
-        for (int rep = 0; rep < 3; ++rep) {
-            hipLaunchKernelGGL(sim_probe, 1, threads, 0, 0, db, dr, G, H, F, cyc, out);
-            uint64_t c = 0;
-            (void)hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
-            if (rep == 2)
-                printf("{\"threads\": %d, \"jobs_per_lane\": %u, \"cycles\": %llu, \"cycles_per_job\": %.1f}\n", threads,
-                       (J + 7) / 8, (unsigned long long)c, (double)c / ((J + 7) / 8));
+        for (uint32_t nc : {1u, 8u, 16u, 28u, 44u}) {
+            if (nc * 8 > (uint32_t)threads) continue;
+            for (int rep = 0; rep < 3; ++rep) {
+                hipLaunchKernelGGL(sim_probe, 1, threads, 0, 0, db, dr, G, H, F, nc, cyc, out);
+                uint64_t c = 0;
+                (void)hipMemcpy(&c, cyc, 8, hipMemcpyDeviceToHost);
+                if (rep == 2)
+                    printf("{\"threads\": %d, \"candidates\": %u, \"jobs_per_lane\": %u, \"cycles\": %llu, "
+                           "\"cycles_per_job\": %.1f}\n",
+                           threads, nc, (J + 7) / 8, (unsigned long long)c, (double)c / ((J + 7) / 8));
+            }
         }
     }
     return 0;
