@@ -77,8 +77,10 @@ hipError_t launch_compare(const uint8_t* dig, const uint8_t* exp, uint32_t n, ui
                           hipStream_t st);
 
 // Longest-first order of a ragged batch (sha1_sort.hip): *d_order receives n
-// indices sorted by d_len descending, *d_sorted_len the lengths in that
-// order and *d_plan the mixed kernel's plan area of the same allocation
+// indices in descending order of SHA-1 block count (stable), *d_sorted_len
+// the lengths in that order at each group's first position (64g; the
+// planner reads no other) and *d_plan the mixed kernel's plan area of the
+// same allocation
 // (mixed_plan_bytes(n): 256 bytes of plan words, then the planner's layout
 // summary); release *scratch with hipFreeAsync on the same stream after the
 // consuming kernel has been enqueued.
@@ -89,3 +91,6 @@ inline size_t mixed_plan_bytes(uint32_t n) {
 hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t** d_order,
                                const uint32_t** d_sorted_len, uint32_t** d_plan, void** scratch,
                                hipStream_t st);
+// out[i] = len[order[i]] for every i (diagnostics: s1be_sort_order_async).
+hipError_t gather_sorted_lengths(const uint32_t* d_len, const uint32_t* d_order, uint32_t* d_out, uint32_t n,
+                                 hipStream_t st);

@@ -365,7 +365,7 @@ __device__ __forceinline__ uint32_t group_blocks(const uint32_t* sorted_len, uin
 constexpr uint32_t kSimMaxG = 16384;  // groups whose blocks the planner keeps in LDS
 
 __device__ __forceinline__ uint32_t plan_blocks(const uint32_t* sorted_len, const uint32_t* blocks, uint32_t g) {
-    return g < kSimMaxG ? blocks[g] : group_blocks(sorted_len, g);
+    return g < kSimMaxG ? blocks[g] & 0x0fffffffu : group_blocks(sorted_len, g);  // bits 28-31: the run (sim_xcd)
 }
 
 // Whether group g's chunks lie together: the rule fused_coop_body applies
@@ -514,6 +514,27 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
     return r;
 }
 
+// Job j's duration from its group's word (blocks, run in bits 28-31): the
+// split constant while j < Hs, then the fused one by whether the job's F
+// groups lie together; the fp32 product rounded before the insert's add.
+__device__ __forceinline__ float sim_dur(uint32_t v, uint32_t j, uint32_t Hs, uint32_t F, float cs, float cT,
+                                         float cS) {
+#pragma clang fp contract(off)
+    const uint32_t b = v & 0x0fffffffu, r = v >> 28;
+    const float c = j < Hs ? cs : (r >= F ? cT : cS);
+    return (float)b * c;
+}
+
+// A job of duration d on the CU that frees first: t ascending, the new t[i]
+// is the job's end clamped to [t[i], t[i+1]].
+__device__ __forceinline__ void sim_insert(uint32_t (&t)[kSimCus], float d) {
+#pragma clang fp contract(off)
+    const uint32_t nx = __float_as_uint(__uint_as_float(t[0]) + d);
+#pragma unroll
+    for (uint32_t i = 0; i + 1 < kSimCus; ++i) t[i] = umed3(t[i], nx, t[i + 1]);
+    t[kSimCus - 1] = max(t[kSimCus - 1], nx);
+}
+
 // Jobs x, x + 8, .. of a plan on one XCD's `per` CUs: the time its last CU
 // frees.  t holds the free times in ascending order (+inf past `per`); a
 // job starts at t[0] and its end is inserted in order.  Simulated only for
@@ -527,11 +548,10 @@ __device__ __forceinline__ uint32_t umed3(uint32_t a, uint32_t b, uint32_t c) {
 // Branch-free, with the next job's two LDS reads in flight during this
 // job's insert: the lanes of a wave simulate different candidates, and a
 // per-mode branch with its own read and wait (round 4) cost ~3x this.
-__device__ float sim_xcd(const uint32_t* blocks, const PlanLayout& L, uint32_t G, uint32_t mode, uint32_t H,
+__device__ __forceinline__ float sim_xcd(const uint32_t* blocks, const PlanLayout& L, uint32_t G, uint32_t mode, uint32_t H,
                          uint32_t F, uint32_t x, uint32_t per) {
 #pragma clang fp contract(off)
     typedef const volatile __attribute__((address_space(3))) uint32_t lds_u32;
-    typedef const volatile __attribute__((address_space(3))) uint8_t lds_u8v;
     // Free times as the bits of non-negative floats, which order as
     // unsigned integers (+inf above every finite time), so the insert is
     // v_med3_u32: ~205 shader cycles per job against ~300 for v_med3_f32 and
@@ -544,24 +564,40 @@ __device__ float sim_xcd(const uint32_t* blocks, const PlanLayout& L, uint32_t G
     const uint32_t Hs = mode == 1 ? J : H, m = mode == 1 ? 2u : 1u;
     const float cs = mode == 1 ? kChainSplit8f : kChainSplit4f;
     const float cT = F == 8 ? kChainFused8Tf : kChainFused4Tf, cS = F == 8 ? kChainFused8Sf : kChainFused4Sf;
-    auto group = [&](uint32_t j) { return j < Hs ? m * j : Hs + (j - Hs) * F; };
-    uint32_t b = 0, r = 0;
+    // g = m*j while j < Hs, Hs + (j - Hs)*F after (m, F powers of two; mode 1
+    // never leaves the first phase): shifts, min and max, no branch (the
+    // ternary compiled to two branches and a 64-bit multiply per job, which
+    // doubled the insert's ~265 cycles, profiles/fixed_cost_planner_r05.log)
+    const uint32_t msh = m == 2u ? 1u : 0u, fsh = F == 8u ? 3u : 2u;
+    auto group = [&](uint32_t j) { return (min(j, Hs) << msh) + ((max(j, Hs) - Hs) << fsh); };
+    // each group's blocks with its run in bits 28-31 (one read per job), two
+    // jobs ahead: with 44 candidates' lanes reading distinct addresses, one
+    // job's insert did not cover the reads (~470 cycles per job in the
+    // planner against ~265 in tools/sim_probe.hip)
+    auto read = [&](uint32_t j) { return *(lds_u32*)(&blocks[group(j)]); };
+    uint32_t va = 0, vb = 0;
     if (x < J) {
-        const uint32_t g = group(x);
-        b = *(lds_u32*)(&blocks[g]);
-        r = *(lds_u8v*)(&L.run[g]);
+        va = read(x);
+        vb = read(x + kSimXcds < J ? x + kSimXcds : x);
     }
-    for (uint32_t j = x; j < J; j += kSimXcds) {
-        const float c = j < Hs ? cs : (r >= F ? cT : cS);
-        const float d = (float)b * c;
-        const uint32_t g = group(j + kSimXcds < J ? j + kSimXcds : j);  // the next job (this one past the end)
-        b = *(lds_u32*)(&blocks[g]);
-        r = *(lds_u8v*)(&L.run[g]);
-        const uint32_t nx = __float_as_uint(__uint_as_float(t[0]) + d);
-        // t ascending: the new t[i] is nx clamped to [t[i], t[i+1]]
-#pragma unroll
-        for (uint32_t i = 0; i + 1 < kSimCus; ++i) t[i] = umed3(t[i], nx, t[i + 1]);
-        t[kSimCus - 1] = max(t[kSimCus - 1], nx);
+    // job j from v (its group's word), whose register then takes the job two
+    // ahead (a job of this lane's past the end); two jobs per iteration so
+    // the two words alternate with no register copy (a copy waited for the
+    // newest read)
+    for (uint32_t j = x; j < J; j += 2u * kSimXcds) {
+        {
+            const float d = sim_dur(va, j, Hs, F, cs, cT, cS);
+            va = read(j + 2u * kSimXcds < J ? j + 2u * kSimXcds : j);
+            sim_insert(t, d);
+        }
+        {  // past the end a job of duration 0, which ends at t[0]: no change
+            // (unconditional, so both reads are always in flight and the wait
+            // before the first step is for the older one only)
+            const uint32_t k = j + kSimXcds < J ? j + kSimXcds : j;
+            const float d = j + kSimXcds < J ? sim_dur(vb, k, Hs, F, cs, cT, cS) : 0.0f;
+            vb = read(k + 2u * kSimXcds < J ? k + 2u * kSimXcds : k);
+            sim_insert(t, d);
+        }
     }
     uint32_t last = 0u;
 #pragma unroll
@@ -591,8 +627,9 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     const uint32_t n = A.n;
     const uint32_t t = threadIdx.x;
     if (t == 0) plan[3] = 0u;  // the persistent kernel's job counter
-    // stage end times (s_memrealtime, 100 MHz; plan[8..13], thread 0) for
-    // SHA1CHUNK_MIXED_DEBUG: scan, bounds search, passes 1, 2, 3
+    // stage end times (s_memrealtime, 100 MHz; plan[8..12], thread 0) for
+    // SHA1CHUNK_MIXED_DEBUG: scan, bounds search, the first simulation
+    // sweep, pass 2's rest, pass 3's misses
     uint64_t ts[6] = {0, 0, 0, 0, 0, 0};
     // and the shader-clock cycles at the same points (plan[14..18])
     uint64_t cs[6] = {0, 0, 0, 0, 0, 0};
@@ -664,6 +701,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
             if (!tg) break;
         }
         run8[g] = static_cast<uint8_t>(r);
+        blocks[g] |= r << 28;  // for sim_xcd, one LDS read per job (blocks < 2^27)
     }
     __syncthreads();
     const PlanLayout L{run8, ft >= 0.5};
@@ -757,12 +795,17 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     // below G, 8.  Wave 0 builds the list in parallel (positions from
     // ballots), then each candidate's makespan bounds are computed once.
     constexpr uint32_t kMaxCand = kPlanThreads / kSimXcds;
-    constexpr uint32_t kSpec = 32;  // heads hb -/+ 1..16, simulated in the first sweep
+    // heads hb -/+ 1..12 simulated in the first sweep: with the bounds' plan
+    // and the near candidates they are <= 32 candidates, four waves, one per
+    // SIMD (44 candidates put two waves on some SIMDs: 38.6 against 25.4
+    // kcycles, tools/sim_probe.hip, profiles/sim_probe2_r05.log)
+    constexpr uint32_t kSpec = 24;
     __shared__ uint32_t cmode[kMaxCand], chead[kMaxCand], cf[kMaxCand], ncand, nref, npend, nmiss, nrun;
     __shared__ float cmk[kMaxCand], scmk[kSpec];
     __shared__ double clb[kMaxCand];
     __shared__ uint8_t cstate[kMaxCand], sval[kSpec];
     __shared__ uint8_t runidx[kMaxCand];  // the first sweep's work: slot, or 128 + early head
+    __shared__ uint32_t simcyc;  // debug: the longest simulate call of the first sweep (plan[27])
     const uint32_t hb = best_h[0], fb = best_f[0];
     const double mb = best_m[0];
     auto put = [&](uint32_t k, uint32_t m, uint32_t h, uint32_t f) {
@@ -771,6 +814,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         cf[k] = h == G ? 4u : f;
     };
     if (t < kMaxCand) cstate[t] = 0;
+    if (t == 0) simcyc = 0;
     if (t < 64) {
         // lanes 0..13: the d entries (lane 2q: hb - 2^q, 2q + 1: hb + 2^q);
         // lanes 14..45: grid head i = lane - 14 (at F = 4, and 8 below G)
@@ -825,9 +869,21 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     if (t < 64) {
         uint32_t off = 0;
         for (uint32_t i = t; i < kMaxCand + kSpec; i += 64) {
-            const bool w = i < kMaxCand ? (i == 0 || (i < ncand && clb[i] < early &&
-                                                      plan_jobs(G, cmode[i], chead[i], cf[i]) <= jcap))
-                                        : sval[i - kMaxCand] != 0;
+            bool w = i < kMaxCand ? (i == 0 || (i < ncand && clb[i] < early &&
+                                                plan_jobs(G, cmode[i], chead[i], cf[i]) <= jcap))
+                                  : sval[i - kMaxCand] != 0;
+            if (w && i >= 1u && i < kMaxCand && cmode[i] == 0u && cf[i] == fb) {
+                // the same plan as the bounds' one or an early head: copied
+                // from that one's result after the sweep, not run twice
+                const uint32_t h = chead[i], e = h < hb ? hb - h : h - hb;
+                if (e == 0u) {
+                    cstate[i] = 5;
+                    w = false;
+                } else if (e <= kSpec / 2u && sval[2u * (e - 1u) + (h > hb ? 1u : 0u)]) {
+                    cstate[i] = 4;
+                    w = false;
+                }
+            }
             const uint64_t bal = __ballot(w);
             if (w) {
                 runidx[off + __popcll(bal & ((1ull << t) - 1ull))] = static_cast<uint8_t>(i);
@@ -835,7 +891,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
             }
             off += __popcll(bal);
         }
-        if (t == 0) nrun = off;  // <= 1 + 80 + 32 (kMaxCand + kSpec slots: 160 fit the uint8 indices)
+        if (t == 0) nrun = off;  // <= 1 + 80 + 24 (kMaxCand + kSpec slots fit the uint8 indices)
     }
     __syncthreads();
     if (t == 0) sub[2] = __builtin_amdgcn_s_memtime();
@@ -859,7 +915,10 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         const uint32_t sm = main ? cmode[i] : 0u, sh = main ? chead[i] : ((q & 1u) == 0u ? hb - d : hb + d);
         const uint32_t sf = main ? cf[i] : fb;
         float mk = __builtin_inff();
+        const uint64_t w0 = __builtin_amdgcn_s_memtime();
         if (run) mk = sim_xcd(blocks, L, G, sm, sh, sf, x, xcus);
+        const uint64_t w1 = __builtin_amdgcn_s_memtime();
+        if (run && (t & 63u) == 0u) atomicMax(&simcyc, static_cast<uint32_t>(w1 - w0));
 #pragma unroll
         for (uint32_t m = 1; m < kSimXcds; m *= 2) mk = fmaxf(mk, __shfl_xor(mk, m));
         if (x == 0 && run) {
@@ -877,6 +936,11 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     // pass 2's rule: bounds at or above the bounds' plan's simulated time
     // rule a candidate out (cmk = inf, simulated early or not)
     if (t >= 1 && t < ncand) {
+        if (cstate[t] >= 4) {  // a copy of the bounds' plan or of an early head
+            const uint32_t h = chead[t], e = h < hb ? hb - h : h - hb;
+            cmk[t] = cstate[t] == 5 ? cmk[0] : scmk[2u * (e - 1u) + (h > hb ? 1u : 0u)];
+            cstate[t] = 3;
+        }
         if (!(clb[t] < (double)cmk[0])) {
             cmk[t] = __builtin_inff();
         } else if (cstate[t] != 3) {
@@ -991,6 +1055,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         plan[23] = nrun;
 #pragma unroll
         for (int i = 0; i < 3; ++i) plan[24 + i] = static_cast<uint32_t>(bsub[i] - cs[0]);
+        plan[27] = simcyc;
     }
 }
 

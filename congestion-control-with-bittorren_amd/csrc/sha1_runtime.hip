@@ -370,19 +370,20 @@ int launch_mixed_checked(const BatchArgs& A, const uint32_t* sorted_len, uint32_
     hipError_t e = launch_mixed(A, sorted_len, plan, cus, force ? forced : nullptr, st);
     if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "mixed kernel launch: %s", hipGetErrorString(e));
     if (const char* d = getenv("SHA1CHUNK_MIXED_DEBUG"); d && atoi(d)) {
-        uint32_t p[27];
+        uint32_t p[28];
         HIP_TRY(hipMemcpyAsync(p, plan, sizeof p, hipMemcpyDeviceToHost, st));
         HIP_TRY(hipStreamSynchronize(st));
         fprintf(stderr, "sha1chunk mixed plan: n=%u groups=%u cus=%d mode=%u H=%u F=%u\n", A.n,
                 (A.n + 63u) / 64u, cus, p[0], p[1], p[2]);
-        if (!force && p[12])  // the planner's stage end times (us since its start)
+        if (!force && p[12])  // the planner's stage end times (us since its start; the first
+                              // simulation sweep, pass 2's rest, pass 3's misses) and shader kcycles
             fprintf(stderr,
-                    "sha1chunk mixed planner stages: scan %.1f bounds %.1f sim1 %.1f sim2 %.1f sim3 %.1f us;"
+                    "sha1chunk mixed planner stages: scan %.1f bounds %.1f sweep %.1f pass2 %.1f pass3 %.1f us;"
                     " kcycles %.1f %.1f %.1f %.1f %.1f (bounds: run8 %.1f prefix %.1f search %.1f; first sweep:"
-                    " list %.1f bounds %.1f packed %.1f, %u candidates)\n",
+                    " list %.1f bounds %.1f packed %.1f, %u candidates, longest call %.1f)\n",
                     p[8] * 0.01, p[9] * 0.01, p[10] * 0.01, p[11] * 0.01, p[12] * 0.01, p[14] * 1e-3, p[15] * 1e-3,
                     p[16] * 1e-3, p[17] * 1e-3, p[18] * 1e-3, p[24] * 1e-3, p[25] * 1e-3, p[26] * 1e-3,
-                    p[20] * 1e-3, p[21] * 1e-3, p[22] * 1e-3, p[23]);
+                    p[20] * 1e-3, p[21] * 1e-3, p[22] * 1e-3, p[23], p[27] * 1e-3);
     }
     return SHA1CHUNK_OK;
 }
@@ -731,9 +732,9 @@ int s1be_sort_order_async(const uint32_t* d_lengths, size_t n, uint32_t* d_order
     void* scratch = nullptr;
     hipError_t e = sort_by_length_desc(d_lengths, static_cast<uint32_t>(n), &order, &sorted_len, &plan, &scratch, st);
     if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "length sort: %s", hipGetErrorString(e));
+    (void)sorted_len;  // group heads only: every position's length is gathered below
     e = hipMemcpyAsync(d_order, order, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
-    if (e == hipSuccess)
-        e = hipMemcpyAsync(d_sorted_len, sorted_len, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess) e = gather_sorted_lengths(d_lengths, order, d_sorted_len, static_cast<uint32_t>(n), st);
     (void)hipFreeAsync(scratch, st);
     if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "sort copy: %s", hipGetErrorString(e));
     return SHA1CHUNK_OK;

@@ -20,7 +20,7 @@
 //                    own launch: global atomics from the scatter serialised,
 //                    40 against 24 us at 131072 chunks in arrival order)
 //   sort_scatter<2>  stable scatter by the high digit: the order, and the
-//                    sorted lengths the planner reads
+//                    sorted lengths the planner reads (each group's first)
 // A tile's start for digit d is the count of d in the tiles before it plus
 // every larger digit's total, each workgroup summing the histogram columns
 // itself (T / 4 loads per thread), so no scan launch.  Inside a tile, rank =
@@ -222,7 +222,9 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint16_t* key
                 ids_out[dst] = id[it];
             } else {
                 ids_out[dst] = id[it];
-                sorted_len[dst] = len[id[it]];
+                // the planner reads a group's first length only (group_blocks):
+                // one gather in 64, not every chunk's
+                if ((dst & 63u) == 0u) sorted_len[dst] = len[id[it]];
             }
         }
     }
@@ -305,4 +307,11 @@ hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t
     *d_plan = plan;
     *scratch = mem;
     return hipSuccess;
+}
+
+hipError_t gather_sorted_lengths(const uint32_t* d_len, const uint32_t* d_order, uint32_t* d_out, uint32_t n,
+                                 hipStream_t st) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(gather_lengths, dim3((n + 255u) / 256u), dim3(256), 0, st, d_len, d_order, d_out, n);
+    return hipGetLastError();
 }

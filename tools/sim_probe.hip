@@ -19,14 +19,20 @@ __global__ __launch_bounds__(1024) void sim_probe(const uint32_t* gblocks, const
     }
     __syncthreads();
     const PlanLayout L{run8, false};
+    __shared__ uint32_t longest;
+    if (threadIdx.x == 0) longest = 0;
+    __syncthreads();
     const uint32_t t = threadIdx.x, c = t / kSimXcds, x = t % kSimXcds;
+    // per-lane runtime mode and F, as in the planner (gblocks[G + c] = 0 / 8)
+    const uint32_t mode = gblocks[G] & 0u, f = c & 1u ? F : F;
     const uint64_t c0 = __builtin_amdgcn_s_memtime();
     float mk = 0.0f;
-    if (c < ncand) mk = sim_xcd(blocks, L, G, 0, H - 8u + c % 17u, F, x, kSimCus);
+    if (c < ncand) mk = sim_xcd(blocks, L, G, mode, H - 8u + c, f, x, kSimCus);
     const uint64_t c1 = __builtin_amdgcn_s_memtime();
+    if (c < ncand && (t & 63u) == 0u) atomicMax(&longest, static_cast<uint32_t>(c1 - c0));
     __syncthreads();
     out[t] = mk;
-    if (t == 0) *cyc = c1 - c0;
+    if (t == 0) *cyc = longest;
 }
 
 int main() {
@@ -38,11 +44,12 @@ int main() {
     uint8_t* dr;
     uint64_t* cyc;
     float* out;
-    (void)hipMalloc(&db, G * 4);
+    (void)hipMalloc(&db, (G + 1) * 4);
     (void)hipMalloc(&dr, G);
     (void)hipMalloc(&cyc, 8);
     (void)hipMalloc(&out, 1024 * 4);
-    (void)hipMemcpy(db, b.data(), G * 4, hipMemcpyHostToDevice);
+    b.push_back(0u);
+    (void)hipMemcpy(db, b.data(), (G + 1) * 4, hipMemcpyHostToDevice);
     (void)hipMemcpy(dr, r.data(), G, hipMemcpyHostToDevice);
     const uint32_t J = H + (G - H + F - 1) / F;
     for (int threads : {64, 1024}) {
