@@ -59,9 +59,9 @@ def check(sort_order, lens):
     assert np.array_equal(srt, lens[w].astype(np.uint32))
 
 
-@pytest.mark.parametrize("n", [65, 4095, 4096, 4097, 8192 + 63, 131072, 262144 + 4093])
+@pytest.mark.parametrize("n", [65, 4095, 4096, 4097, 8192 + 63, 131072, 262144 + 4093, 1 << 20])
 def test_config5_law_and_tile_edges(sort_order, n):
-    rng = np.random.default_rng(n)
+    rng = np.random.default_rng(n)  # 1 << 20: 256 tiles, the own sort's largest batch
     lens = np.exp(rng.uniform(np.log(4096), np.log(1 << 20), n)).astype(np.uint32)
     lens[rng.choice(n, min(n, 40), replace=False)] = 0
     lens[rng.choice(n, min(n, 40), replace=False)] = 55   # 1 block
