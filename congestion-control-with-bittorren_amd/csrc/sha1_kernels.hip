@@ -545,11 +545,11 @@ __device__ __forceinline__ void sim_insert(uint32_t (&t)[kSimCus], float d) {
 // group's blocks times the shape's chain constant (fused: by whether the F
 // groups from g lie together), the fp32 product rounded before the add
 // (contract off; tests/test_gpu_mixed.py restates it bit for bit).
-// Branch-free, with the next job's two LDS reads in flight during this
-// job's insert: the lanes of a wave simulate different candidates, and a
-// per-mode branch with its own read and wait (round 4) cost ~3x this.
-__device__ __forceinline__ float sim_xcd(const uint32_t* blocks, const PlanLayout& L, uint32_t G, uint32_t mode, uint32_t H,
-                         uint32_t F, uint32_t x, uint32_t per) {
+// Branch-free (the lanes of a wave simulate different candidates, and a
+// per-mode branch with its own read and wait, round 4's form, cost ~3x
+// this), one LDS word per job read ahead of the insert before it.
+__device__ __forceinline__ float sim_xcd(const uint32_t* blocks, uint32_t G, uint32_t mode, uint32_t H, uint32_t F,
+                                         uint32_t x, uint32_t per) {
 #pragma clang fp contract(off)
     typedef const volatile __attribute__((address_space(3))) uint32_t lds_u32;
     // Free times as the bits of non-negative floats, which order as
@@ -571,9 +571,9 @@ __device__ __forceinline__ float sim_xcd(const uint32_t* blocks, const PlanLayou
     const uint32_t msh = m == 2u ? 1u : 0u, fsh = F == 8u ? 3u : 2u;
     auto group = [&](uint32_t j) { return (min(j, Hs) << msh) + ((max(j, Hs) - Hs) << fsh); };
     // each group's blocks with its run in bits 28-31 (one read per job), two
-    // jobs ahead: with 44 candidates' lanes reading distinct addresses, one
-    // job's insert did not cover the reads (~470 cycles per job in the
-    // planner against ~265 in tools/sim_probe.hip)
+    // jobs ahead (measured the same as one: 43.0 against 43.2 kcycles for
+    // the longest call; what had slowed the sweep to ~470 cycles per job was
+    // two waves per SIMD, see plan_mixed_kernel's first sweep)
     auto read = [&](uint32_t j) { return *(lds_u32*)(&blocks[group(j)]); };
     uint32_t va = 0, vb = 0;
     if (x < J) {
@@ -608,7 +608,7 @@ __device__ __forceinline__ float sim_xcd(const uint32_t* blocks, const PlanLayou
 
 // One workgroup, two stages.  Bounds: every mode-0 plan (H in [0, hcap] or
 // H = G, F in {4, 8}) gets the makespan bounds above, the smallest wins
-// (ties: smaller H).  Simulation (up to kSimMaxG groups on 8 XCDs of <= 32
+// (ties: smaller H, then F = 4).  Simulation (up to kSimMaxG groups on 8 XCDs of <= 32
 // CUs): ~80 candidates around it are simulated and the shortest wins, or
 // all-split within 0.5 % of it; beyond that, the bounds' plan or mode 1 by
 // the same bounds.  The plan depends on the lengths and, through the fused
@@ -916,7 +916,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
         const uint32_t sf = main ? cf[i] : fb;
         float mk = __builtin_inff();
         const uint64_t w0 = __builtin_amdgcn_s_memtime();
-        if (run) mk = sim_xcd(blocks, L, G, sm, sh, sf, x, xcus);
+        if (run) mk = sim_xcd(blocks, G, sm, sh, sf, x, xcus);
         const uint64_t w1 = __builtin_amdgcn_s_memtime();
         if (run && (t & 63u) == 0u) atomicMax(&simcyc, static_cast<uint32_t>(w1 - w0));
 #pragma unroll
@@ -952,7 +952,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     if (npend) {
         const bool run = c < ncand && cstate[c] == 1;
         float mk = __builtin_inff();
-        if (run) mk = sim_xcd(blocks, L, G, cmode[c], chead[c], cf[c], x, xcus);
+        if (run) mk = sim_xcd(blocks, G, cmode[c], chead[c], cf[c], x, xcus);
 #pragma unroll
         for (uint32_t m = 1; m < kSimXcds; m *= 2) mk = fmaxf(mk, __shfl_xor(mk, m));
         if (x == 0 && run) cmk[c] = mk;
@@ -1017,7 +1017,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     if (nmiss) {
         const bool run = c >= ncand && c < nref && cstate[c] == 2;
         float mk = __builtin_inff();
-        if (run) mk = sim_xcd(blocks, L, G, cmode[c], chead[c], cf[c], x, xcus);
+        if (run) mk = sim_xcd(blocks, G, cmode[c], chead[c], cf[c], x, xcus);
 #pragma unroll
         for (uint32_t m = 1; m < kSimXcds; m *= 2) mk = fmaxf(mk, __shfl_xor(mk, m));
         if (x == 0 && run) cmk[c] = mk;

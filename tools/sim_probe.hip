@@ -11,14 +11,9 @@
 
 __global__ __launch_bounds__(1024) void sim_probe(const uint32_t* gblocks, const uint8_t* grun, uint32_t G, uint32_t H,
                                                   uint32_t F, uint32_t ncand, uint64_t* cyc, float* out) {
-    __shared__ uint32_t blocks[kSimMaxG];
-    __shared__ uint8_t run8[kSimMaxG];
-    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) {
-        blocks[g] = gblocks[g];
-        run8[g] = grun[g];
-    }
+    __shared__ uint32_t blocks[kSimMaxG];  // as the planner keeps them: the run in bits 28-31
+    for (uint32_t g = threadIdx.x; g < G; g += blockDim.x) blocks[g] = gblocks[g] | (uint32_t)grun[g] << 28;
     __syncthreads();
-    const PlanLayout L{run8, false};
     __shared__ uint32_t longest;
     if (threadIdx.x == 0) longest = 0;
     __syncthreads();
@@ -27,7 +22,7 @@ __global__ __launch_bounds__(1024) void sim_probe(const uint32_t* gblocks, const
     const uint32_t mode = gblocks[G] & 0u, f = c & 1u ? F : F;
     const uint64_t c0 = __builtin_amdgcn_s_memtime();
     float mk = 0.0f;
-    if (c < ncand) mk = sim_xcd(blocks, L, G, mode, H - 8u + c, f, x, kSimCus);
+    if (c < ncand) mk = sim_xcd(blocks, G, mode, H - 8u + c, f, x, kSimCus);
     const uint64_t c1 = __builtin_amdgcn_s_memtime();
     if (c < ncand && (t & 63u) == 0u) atomicMax(&longest, static_cast<uint32_t>(c1 - c0));
     __syncthreads();
