@@ -149,6 +149,7 @@ def test_front_end_links_libc_only(built):
                           text=True).stdout.split()
     assert not [s for s in syms if s.startswith("sha1chunk_") or s in ("shahash", "SHA1Init")]
     assert "s1be_hash_batch" in syms
+    assert "s1be_sort_order_async" in syms  # diagnostics for tests/test_gpu_sort.py
 
 
 def test_missing_backend_fails_loudly(tmp_path, built):
