@@ -406,6 +406,54 @@ def test_mixed_planner_config5_law_131072(pkg, dev, oracle, cus, monkeypatch, ca
     torch.cuda.empty_cache()
 
 
+@pytest.mark.parametrize("seed", range(10))
+def test_mixed_planner_fuzz_against_model(pkg, dev, cus, monkeypatch, capfd, seed):
+    """Random batches through the round-5 planner (packed first sweep, the
+    rest only when needed): 1.2-40 groups per CU, log-uniform, two-level
+    or uniform-random lengths, laid out in arrival order, longest-first or
+    shuffled; the device's plan must simulate no slower than the model's
+    best (the model restates passes 1-3 in order; ties as in
+    test_mixed_planner_matches_model)."""
+    torch = dev
+    rng = np.random.default_rng(7000 + seed)
+    n = int(64 * cus * rng.uniform(1.2, 40.0))
+    law = seed % 3
+    if law == 0:
+        lens = (4096 * 2.0 ** rng.uniform(-3, 6, n)).astype(np.uint32)
+    elif law == 1:
+        lens = np.where(rng.uniform(size=n) < rng.uniform(0.02, 0.3), 1 << 18, 2048).astype(np.uint32)
+    else:
+        lens = rng.integers(0, 65536, n).astype(np.uint32)
+    layout = ("arrival", "longest_first", "shuffled")[(seed // 3) % 3]
+    order = np.arange(n)
+    if layout == "longest_first":
+        order = np.argsort(-np.minimum((lens.astype(np.int64) + 9 + 63) // 64, 65535), kind="stable")
+    elif layout == "shuffled":
+        order = rng.permutation(n)
+    step = (lens[order].astype(np.uint64) + 63) // 64 * 64
+    off = np.zeros(n, np.uint64)
+    off[order] = np.concatenate([[0], np.cumsum(step)[:-1]]).astype(np.uint64)
+    base = torch.zeros(int((off + lens).max()) + 64, dtype=torch.uint8, device="cuda")
+    for k in ("SHA1CHUNK_MIXED_PLAN", "SHA1CHUNK_MIXED"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("SHA1CHUNK_MIXED_DEBUG", "1")
+    dig = torch.zeros((n, 20), dtype=torch.uint8, device="cuda")
+    pkg.hash_device(base, torch.from_numpy(off.astype(np.int64)).cuda(),
+                    torch.from_numpy(lens.astype(np.int32)).cuda(), dig)
+    torch.cuda.synchronize()
+    mode, H, F = _device_plan(capfd)
+    (best, bmode, bH, bF), (B, P, L) = model_plan(lens, cus, offsets=off.astype(np.int64))
+    simulated = len(B) <= SIM_MAX_G and cus % SIM_XCDS == 0 and cus // SIM_XCDS <= SIM_CUS
+    got = float(sim_plan(B, cus, mode, H, F, L)) if simulated else model_makespan(B, cus, mode, H, F, P, L)
+    assert got <= best * (1 + 1e-6), (seed, n, layout, (mode, H, F), got, (bmode, bH, bF), best)
+    d = dig.cpu().numpy()  # zeros: one digest per length
+    for Lb in rng.choice(np.unique(lens), 8):
+        i = int(np.nonzero(lens == Lb)[0][0])
+        assert d[i].tobytes() == hashlib.sha1(bytes(int(Lb))).digest()
+    del base
+    torch.cuda.empty_cache()
+
+
 def test_mixed_beyond_simulated_group_count(pkg, dev, oracle, cus, monkeypatch, capfd, dispatch):
     """More groups than the planner keeps in LDS (SIM_MAX_G = 16384): the
     bounds-only plan, a grid of G workgroups, every digest against the
