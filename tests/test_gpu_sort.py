@@ -90,3 +90,23 @@ def test_rocprim_path_beyond_1mi(sort_order):
     lens = rng.integers(0, 300000, n).astype(np.uint32)
     lens[rng.choice(n, 1000, replace=False)] = 1 << 23
     check(sort_order, lens)
+
+
+@pytest.mark.parametrize("pattern", ["sawtooth", "tile_runs", "alternating", "one_long"])
+def test_adversarial_patterns(sort_order, pattern):
+    """Key patterns that stress the ranking and the per-tile histograms:
+    a sawtooth whose period is not the tile's, one key per tile (every
+    tile's histogram a single slot), two keys alternating lane by lane
+    (every ballot split), and one long chunk among equal short ones."""
+    n = 64 * 1111 + 1
+    i = np.arange(n, dtype=np.int64)
+    if pattern == "sawtooth":
+        lens = (i % 777) * 64 + 1
+    elif pattern == "tile_runs":
+        lens = (i // 4096) * 6400 + 100
+    elif pattern == "alternating":
+        lens = np.where(i % 2 == 0, 100, 1 << 20)
+    else:
+        lens = np.full(n, 64)
+        lens[n // 2] = 1 << 22
+    check(sort_order, lens.astype(np.uint32))
