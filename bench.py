@@ -411,9 +411,8 @@ def _strong_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden):
         dist.barrier()
     wall, kern_ms = shard.max_over_ranks([wall, kern_ms], device=cdev)
     got = dig[:cnt].cpu().numpy()
-    aggs = golden["config4"]["shard_aggs"].get(str(world)) if total == golden["config4"]["chunks"] \
-        else None
-    ok = aggs is not None and hashlib.sha1(got.tobytes()).hexdigest() == aggs[rank]
+    want = shard.strong_golden_agg(golden, world, rank, total)
+    ok = want is not None and hashlib.sha1(got.tobytes()).hexdigest() == want
     parity = shard.all_ranks_ok(ok, device=cdev)
     del buf, dig
     torch.cuda.empty_cache()
@@ -507,9 +506,7 @@ def _weak4_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden):
     way.  Timed like the other legs (3 untimed launches, barrier + synchronize
     around K, max over ranks)."""
     per, L, K = a.weak4_chunks, CHUNK_LEN, max(1, a.strong_steps)
-    c4 = golden["config4"]
-    first, _, k_idx = shard.weak_golden_shard(rank, per, c4["chunks"])
-    aggs = c4["shard_aggs"].get(str(c4["chunks"] // per)) if k_idx is not None else None
+    first, _, want = shard.weak_golden_agg(golden, rank, per)
     st = torch.cuda.Stream()
     buf = torch.empty(per * L, dtype=torch.uint8, device="cuda")
     dig = torch.zeros((per, 20), dtype=torch.uint8, device="cuda")
@@ -521,7 +518,7 @@ def _weak4_leg(pkg, shard, torch, dist, world, rank, cdev, a, golden):
     if world > 1:
         dist.barrier()
     wall, kern_ms = shard.max_over_ranks([wall, kern_ms], device=cdev)
-    ok = aggs is not None and hashlib.sha1(dig.cpu().numpy().tobytes()).hexdigest() == aggs[k_idx]
+    ok = want is not None and hashlib.sha1(dig.cpu().numpy().tobytes()).hexdigest() == want
     parity = shard.all_ranks_ok(ok, device=cdev)
     del buf, dig
     torch.cuda.empty_cache()

@@ -655,8 +655,6 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     uint64_t local = 0, local_t = 0;
     __shared__ uint32_t blocks[kSimMaxG];  // group_blocks of groups < kSimMaxG, for the simulation
     __shared__ uint32_t togw[kSimMaxG / 32];  // plan_layout_kernel's bits, groups < kSimMaxG
-    __shared__ uint64_t tog_blocks;
-    if (t == 0) tog_blocks = 0;
     for (uint32_t g = g0; g < g1; ++g) {
         const uint32_t b = group_blocks(sorted_len, g);
         if (g < kSimMaxG) blocks[g] = b;
@@ -671,6 +669,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     // the 16 wave totals (Hillis-Steele over the workgroup took 20 barriers)
     const uint32_t lane = t & 63u, wv = t >> 6;
     __shared__ uint64_t wtot[kPlanThreads / 64];
+    __shared__ uint64_t wtog[kPlanThreads / 64];  // per-wave toggled-block sums, added after the barrier
     uint64_t inc = local;
 #pragma unroll
     for (uint32_t d = 1; d < 64u; d <<= 1) {
@@ -679,13 +678,14 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     }
     for (uint32_t m = 32; m >= 1; m >>= 1) local_t += __shfl_xor(local_t, m);
     if (lane == 63u) wtot[wv] = inc;
-    if (lane == 0u) atomicAdd(reinterpret_cast<unsigned long long*>(&tog_blocks), static_cast<unsigned long long>(local_t));
+    if (lane == 0u) wtog[wv] = local_t;
     __syncthreads();
-    uint64_t before = 0, PG = 0;
+    uint64_t before = 0, PG = 0, tog_blocks = 0;
 #pragma unroll
     for (uint32_t w = 0; w < kPlanThreads / 64; ++w) {
         before += w < wv ? wtot[w] : 0ull;
         PG += wtot[w];
+        tog_blocks += wtog[w];
     }
     scan[t] = before + inc;
     const double ft = PG ? (double)tog_blocks / (double)PG : 1.0;

@@ -7,7 +7,7 @@ control-plane ones a benchmark or service needs: a barrier, the max of the
 per-rank times, and the AND of the per-rank parity flags.
 
 Used by bench.py (one process per GPU, torch.distributed over RCCL) and
-covered on CPU by tests/test_distributed.py (gloo, world size 2).
+covered on CPU by tests/test_distributed.py (gloo, world sizes 2 and 8).
 """
 from __future__ import annotations
 
@@ -39,6 +39,29 @@ def weak_golden_shard(rank: int, per_rank: int, total: int) -> tuple[int, int, i
     k = total // per_rank
     first, count = strong_shard(rank % k, k, total)
     return first, count, rank % k
+
+
+def strong_golden_agg(golden: dict, world: int, rank: int, total: int) -> str | None:
+    """The reference golden digest-of-digests of rank `rank`'s strong shard
+    (bench.py's `strong` leg): config 4's `world`-way split when the list is
+    config 4's whole list, else None (no golden for that shape)."""
+    c4 = golden["config4"]
+    if total != c4["chunks"]:
+        return None
+    aggs = c4["shard_aggs"].get(str(world))
+    return aggs[rank] if aggs is not None and 0 <= rank < len(aggs) else None
+
+
+def weak_golden_agg(golden: dict, rank: int, per_rank: int) -> tuple[int, int, str | None]:
+    """bench.py's `weak_config4` leg: rank `rank`'s chunk range
+    (weak_golden_shard over config 4's list) and the golden aggregate of that
+    range, None when per_rank does not divide the list."""
+    c4 = golden["config4"]
+    first, count, k_idx = weak_golden_shard(rank, per_rank, c4["chunks"])
+    if k_idx is None:
+        return first, count, None
+    aggs = c4["shard_aggs"].get(str(c4["chunks"] // per_rank))
+    return first, count, aggs[k_idx] if aggs is not None else None
 
 
 def strong_report(total: int, chunk_len: int, world: int, ms_n: float, kern_ms_n: float,

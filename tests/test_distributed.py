@@ -211,3 +211,104 @@ def test_bench_exits_when_ranks_outnumber_gpus():
     assert r.returncode == 2, r.stderr[-500:]
     assert "one rank per GPU" in r.stderr or "no GPU" in r.stderr
     assert not r.stdout.strip()
+
+
+def _eight_worker(rank, world, port, out_dir, small_golden):
+    """bench.py's control plane at the node's full width (world 8 over gloo,
+    SURVEY 8(e)): shard indices, golden lookups, the real-data parity of a
+    small strong list, max over ranks, the parity AND with one rank failing,
+    and the device-identity check over 8 mocked GPUs."""
+    import hashlib
+    import importlib
+    import json
+    import sys
+    sys.path.insert(0, ROOT)
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
+                            world_size=world)
+    shard = importlib.import_module("congestion-control-with-bittorren_amd.shard")
+    from oracle import oracle as O
+    golden = json.load(open(os.path.join(ROOT, "tests/golden/golden.json")))
+    rec = {}
+    # config 4 strong: 262144 chunks, 32768 per rank, and the golden aggregate
+    # this rank's parity is checked against
+    rec["strong"] = list(shard.strong_shard(rank, world, 262144))
+    rec["strong_agg"] = shard.strong_golden_agg(golden, world, rank, 262144)
+    rec["strong_agg_other_total"] = shard.strong_golden_agg(golden, world, rank, 262143)
+    # config 4 weak: 65536 per rank, shard rank % 4 of the 4-way split
+    first, count, want = shard.weak_golden_agg(golden, rank, 65536)
+    rec["weak"] = [first, count]
+    rec["weak_agg"] = want
+    # real data: a 64-chunk strong list (4 KiB chunks of the same corpus)
+    # split 8 ways, each rank's digests from the oracle, the aggregate
+    # compared exactly as bench.py's strong leg compares it
+    L, total = 4096, 64
+    f, c = shard.strong_shard(rank, world, total)
+    data = O.synth_chunks(f, c, L)
+    dig = O.hash_batch(data, np.arange(c, dtype=np.uint64) * L, np.full(c, L, np.uint32), threads=1)
+    agg = shard.strong_golden_agg(small_golden, world, rank, total)
+    ok = agg is not None and hashlib.sha1(dig.tobytes()).hexdigest() == agg
+    rec["own_ok"] = ok
+    rec["all_ok"] = shard.all_ranks_ok(ok)
+    rec["one_bad"] = shard.all_ranks_ok(ok and rank != 5)
+    rec["max"] = shard.max_over_ranks([0.25 * rank, 7.0 - rank, 3.0])
+    # identities: 8 distinct GPUs, then rank 6 reporting rank 2's card
+    for case in ("distinct", "dup"):
+        ident = shard.device_identity("node0", rank, rank, rank, None)
+        ident["uuid"] = f"GPU-{2 if (case == 'dup' and rank == 6) else rank}"
+        idents = shard.gather_identities(ident)
+        try:
+            shard.check_distinct_devices(idents)
+            rec[case] = "ok"
+        except shard.DeviceMapError as e:
+            rec[case] = str(e)
+        rec[case + "_n"] = len(idents)
+    rep = shard.strong_report(262144, 524288, world, rec["max"][1], rec["max"][2], 38.3, 38.3,
+                              rec["all_ok"], True, 10)
+    rec["report"] = [rep["speedup"], rep["efficiency"], rep["value"], rep["parity"]]
+    with open(os.path.join(out_dir, f"e{rank}.json"), "w") as fh:
+        json.dump(rec, fh)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_eight_rank_control_plane(tmp_path, oracle):
+    """World size 8 (the 8-GPU node's bench launch, rehearsed over gloo on
+    the CPU; VERDICT r5 next #4)."""
+    import hashlib
+    import json
+    world, L, total = 8, 4096, 64
+    golden = json.load(open(os.path.join(ROOT, "tests/golden/golden.json")))
+    # the small list's golden aggregates, from the standard library's SHA-1
+    # over the same corpus bytes (independent of the oracle the ranks use)
+    import importlib
+    shard = importlib.import_module("congestion-control-with-bittorren_amd.shard")
+    data = oracle.synth_chunks(0, total, L)
+    d = b"".join(hashlib.sha1(data[i * L:(i + 1) * L].tobytes()).digest() for i in range(total))
+    aggs = []
+    for r in range(world):
+        f, c = shard.strong_shard(r, world, total)
+        aggs.append(hashlib.sha1(d[20 * f:20 * (f + c)]).hexdigest())
+    small = {"config4": {"chunks": total, "shard_aggs": {str(world): aggs}}}
+    mp.start_processes(_eight_worker, args=(world, _free_port(), str(tmp_path), small), nprocs=world,
+                       join=True, start_method="spawn")
+    recs = [json.load(open(tmp_path / f"e{r}.json")) for r in range(world)]
+    c4 = golden["config4"]
+    for r, rec in enumerate(recs):
+        assert rec["strong"] == [r * 32768, 32768]
+        assert rec["strong_agg"] == c4["shard_aggs"]["8"][r]
+        assert rec["strong_agg_other_total"] is None
+        assert rec["weak"] == [(r % 4) * 65536, 65536]
+        assert rec["weak_agg"] == c4["shard_aggs"]["4"][r % 4]
+        assert rec["own_ok"] and rec["all_ok"]
+        assert rec["one_bad"] is False  # rank 5's False reaches every rank
+        assert rec["max"] == [1.75, 7.0, 3.0]
+        assert rec["distinct"] == "ok" and rec["distinct_n"] == 8
+        assert "ranks 2 and 6 share GPU GPU-2" in rec["dup"] and rec["dup_n"] == 8
+        assert rec["report"] == recs[0]["report"]
+    assert len(set(c4["shard_aggs"]["8"])) == 8
+    # ranks 0 and 4 hash config 3's range: the same golden aggregate
+    assert recs[0]["weak_agg"] == recs[4]["weak_agg"] == golden["config3"]["agg"]
+    sp, eff, val, par = recs[0]["report"]
+    assert sp == pytest.approx(38.3 / 7.0, rel=1e-3) and eff == pytest.approx(sp / 8, rel=1e-3)
+    assert par is True

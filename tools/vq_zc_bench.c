@@ -21,20 +21,35 @@
  * golden digests (tests/golden/synth_4096x512k.bin); every 5th chunk is
  * corrupted in its buffer before the verify and must come back 1.  Prints
  * one JSON line.
+ *
+ * Placement: the line records where the work ran --
+ * the GPU's NUMA node (its PCI device's numa_node), each producer's CPU and
+ * node at its start and end, the node histogram of the queue's data ring
+ * (walked once with reserve/release before the timed run), of the source
+ * chunks and of the submit buffers, and the cgroup's CPU throttling over the
+ * timed region.  --pin gpu binds every producer to the GPU node's CPUs
+ * (within this process's affinity mask) and has each producer write its own
+ * source chunks there (first touch), as a NIC-local receive thread would;
+ * --pin none leaves placement to the scheduler.
  */
 #define _GNU_SOURCE
+#include <ctype.h>
+#include <dirent.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <sys/syscall.h>
 #include <unistd.h>
 
 #include "../include/sha1chunk.h"
 
 #define L512 524288u
 #define PIECE 1484u
+#define MAXNODE 8 /* histograms: nodes 0..7, then "unknown" */
 
 static uint64_t splitmix64(uint64_t x) {
     uint64_t z = x + 0x9E3779B97F4A7C15ull;
@@ -51,6 +66,115 @@ static void synth_chunk(uint8_t *dst, uint64_t chunk) {
     }
 }
 
+/* ---- placement ---------------------------------------------------------- */
+static int cpu_node(int cpu) {
+    char path[96];
+    snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d", cpu);
+    DIR *d = opendir(path);
+    if (!d) return -1;
+    int node = -1;
+    for (struct dirent *e; (e = readdir(d));)
+        if (!strncmp(e->d_name, "node", 4) && isdigit((unsigned char)e->d_name[4])) {
+            node = atoi(e->d_name + 4);
+            break;
+        }
+    closedir(d);
+    return node;
+}
+
+/* node of each page in pages[0..n) (move_pages with no target: a query) */
+static void page_hist(void **pages, size_t n, long *hist) {
+    int *st = (int *)malloc(n * sizeof *st);
+    if (!st) return;
+    const long rc = syscall(SYS_move_pages, 0, (unsigned long)n, pages, NULL, st, 0);
+    for (size_t i = 0; i < n; ++i) {
+        const int v = rc == 0 ? st[i] : -1;
+        hist[v >= 0 && v < MAXNODE ? v : MAXNODE]++;
+    }
+    free(st);
+}
+
+static void range_hist(const uint8_t *p, size_t bytes, size_t step, long *hist) {
+    const size_t n = (bytes + step - 1) / step;
+    void **pg = (void **)malloc(n * sizeof *pg);
+    if (!pg) return;
+    for (size_t i = 0; i < n; ++i) pg[i] = (void *)((uintptr_t)(p + i * step) & ~(uintptr_t)4095);
+    page_hist(pg, n, hist);
+    free(pg);
+}
+
+static void put_hist(FILE *o, const char *name, const long *hist) {
+    fprintf(o, "\"%s\": {", name);
+    int first = 1;
+    for (int k = 0; k <= MAXNODE; ++k)
+        if (hist[k]) {
+            if (k < MAXNODE) fprintf(o, "%s\"%d\": %ld", first ? "" : ", ", k, hist[k]);
+            else fprintf(o, "%s\"unknown\": %ld", first ? "" : ", ", hist[k]);
+            first = 0;
+        }
+    fprintf(o, "}");
+}
+
+/* the GPU's NUMA node: numa_node of its PCI device (-1 unknown) */
+static int gpu_node(char *bdf, size_t len) {
+    if (sha1chunk_device_pci_bus_id(sha1chunk_get_device(), bdf, len) != 0) {
+        snprintf(bdf, len, "?");
+        return -1;
+    }
+    for (char *c = bdf; *c; ++c) *c = (char)tolower((unsigned char)*c);
+    char path[160];
+    snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bdf);
+    FILE *f = fopen(path, "r");
+    int node = -1;
+    if (f) {
+        if (fscanf(f, "%d", &node) != 1) node = -1;
+        fclose(f);
+    }
+    return node;
+}
+
+/* node's CPUs within this process's affinity mask (count of them) */
+static int node_cpus(int node, cpu_set_t *out) {
+    CPU_ZERO(out);
+    if (node < 0) return 0;
+    cpu_set_t allowed;
+    if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return 0;
+    char path[96], buf[4096];
+    snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+    FILE *f = fopen(path, "r");
+    if (!f) return 0;
+    if (!fgets(buf, sizeof buf, f)) buf[0] = 0;
+    fclose(f);
+    for (char *tok = strtok(buf, ",\n"); tok; tok = strtok(NULL, ",\n")) {
+        int a, b;
+        const int k = sscanf(tok, "%d-%d", &a, &b);
+        if (k < 1) continue;
+        if (k == 1) b = a;
+        for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
+            if (CPU_ISSET(c, &allowed)) CPU_SET(c, out);
+    }
+    return CPU_COUNT(out);
+}
+
+/* cgroup CPU throttling counters (v2 cpu.stat; v1 cpu/cpu.stat, ns) */
+static void cg_throttle(long long *nr, long long *usec) {
+    *nr = *usec = -1;
+    const char *paths[2] = {"/sys/fs/cgroup/cpu.stat", "/sys/fs/cgroup/cpu/cpu.stat"};
+    for (int k = 0; k < 2; ++k) {
+        FILE *f = fopen(paths[k], "r");
+        if (!f) continue;
+        char key[64];
+        long long v;
+        while (fscanf(f, "%63s %lld", key, &v) == 2) {
+            if (!strcmp(key, "nr_throttled")) *nr = v;
+            else if (!strcmp(key, "throttled_usec")) *usec = v;
+            else if (!strcmp(key, "throttled_time")) *usec = v / 1000;
+        }
+        fclose(f);
+        return;
+    }
+}
+
 static struct {
     sha1chunk_vq *q;
     int mode; /* 0 reserve, 1 submit, 2 fill */
@@ -63,6 +187,11 @@ static struct {
     pthread_barrier_t start;
     pthread_mutex_t err_mu;
     int errors;
+    int pin;           /* 1: producers on the GPU node's CPUs, source chunks first-touched there */
+    int local_src;     /* producers write their own source chunks */
+    cpu_set_t pin_set;
+    int cpu0[64], cpu1[64];
+    void *own_page[64];
 } B;
 
 static void fail_msg(const char *what) {
@@ -98,8 +227,17 @@ static void fill(uint8_t *dst, const uint8_t *src) {
 
 static void *producer(void *arg) {
     const int t = (int)(intptr_t)arg;
+    if (B.pin) (void)sched_setaffinity(0, sizeof B.pin_set, &B.pin_set);
+    if (B.local_src)
+        for (size_t c = (size_t)t; c < B.distinct; c += (size_t)B.threads)
+            synth_chunk(B.src + c * (size_t)L512, c);
     uint8_t *own = B.mode == 1 ? (uint8_t *)malloc(L512) : NULL;
+    if (own) {
+        memset(own, 0, L512);
+        if (t < 64) B.own_page[t] = own;
+    }
     pthread_barrier_wait(&B.start);
+    if (t < 64) B.cpu0[t] = sched_getcpu();
     size_t since = 0;
     for (size_t i = (size_t)t; i < B.n; i += (size_t)B.threads) {
         const uint8_t *src = B.src + (i % B.distinct) * (size_t)L512;
@@ -131,6 +269,15 @@ static void *producer(void *arg) {
             drain(0);
         }
     }
+    if (t < 64) B.cpu1[t] = sched_getcpu();
+    if (own && t < 64) {
+        long h[MAXNODE + 1] = {0};
+        range_hist(own, L512, 4096, h);
+        int k = MAXNODE;
+        for (int j = 0; j < MAXNODE; ++j)
+            if (h[j]) k = j;
+        B.own_page[t] = (void *)(intptr_t)k;  /* reused: the buffer's node */
+    }
     free(own);
     return NULL;
 }
@@ -138,6 +285,7 @@ static void *producer(void *arg) {
 int main(int argc, char **argv) {
     const char *golden_path = "tests/golden/synth_4096x512k.bin";
     const char *mode = "reserve";
+    const char *pin = "none";
     size_t batch = 64;
     B.n = 16384;
     B.distinct = 256;
@@ -151,6 +299,7 @@ int main(int argc, char **argv) {
         else if (!strcmp(argv[i], "--batch")) batch = strtoull(argv[i + 1], NULL, 10);
         else if (!strcmp(argv[i], "--pieces")) B.pieces = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--golden")) golden_path = argv[i + 1];
+        else if (!strcmp(argv[i], "--pin")) pin = argv[i + 1];
         else {
             fprintf(stderr, "unknown option %s\n", argv[i]);
             return 2;
@@ -158,6 +307,10 @@ int main(int argc, char **argv) {
     }
     B.mode = !strcmp(mode, "submit") ? 1 : (!strcmp(mode, "fill") ? 2 : 0);
     if (B.threads < 1 || B.distinct < 1 || B.distinct > 4096) return 2;
+    if (strcmp(pin, "none") && strcmp(pin, "gpu")) {
+        fprintf(stderr, "--pin none|gpu\n");
+        return 2;
+    }
     B.golden = (uint8_t *)malloc(20 * B.distinct);
     FILE *g = fopen(golden_path, "rb");
     if (!g || fread(B.golden, 20, B.distinct, g) != B.distinct) {
@@ -165,8 +318,15 @@ int main(int argc, char **argv) {
         return 2;
     }
     fclose(g);
+    char bdf[64];
+    const int gnode = gpu_node(bdf, sizeof bdf);
+    const int ncpu_pin = node_cpus(gnode, &B.pin_set);
+    B.pin = !strcmp(pin, "gpu") && ncpu_pin > 0;
+    /* producer t reads chunks c = t mod threads only when threads divides distinct */
+    B.local_src = B.pin && B.distinct % (size_t)B.threads == 0;
     B.src = (uint8_t *)malloc(B.distinct * (size_t)L512);
-    for (size_t c = 0; c < B.distinct; ++c) synth_chunk(B.src + c * (size_t)L512, c);
+    if (!B.local_src)
+        for (size_t c = 0; c < B.distinct; ++c) synth_chunk(B.src + c * (size_t)L512, c);
     B.bufp = (void **)calloc(B.n, sizeof *B.bufp);
     B.result = (volatile uint8_t *)calloc(B.n, 1);
     pthread_mutex_init(&B.err_mu, NULL);
@@ -189,17 +349,36 @@ int main(int argc, char **argv) {
         while (sha1chunk_vq_poll(B.q, tags, mis, 64, 1) > 0) {
         }
     }
+    /* the data ring's pages: walk it once, one reservation after another */
+    long ring_h[MAXNODE + 1] = {0};
+    {
+        const size_t steps = 4096;
+        void **pg = (void **)malloc(steps * 2 * sizeof *pg);
+        size_t np = 0;
+        for (size_t k = 0; k < steps; ++k) {
+            uint8_t *p = (uint8_t *)sha1chunk_vq_reserve(B.q, L512);
+            if (!p) break;
+            pg[np++] = (void *)((uintptr_t)p & ~(uintptr_t)4095);
+            pg[np++] = (void *)((uintptr_t)(p + L512 / 2) & ~(uintptr_t)4095);
+            if (sha1chunk_vq_release(B.q, p) != 0) break;
+        }
+        page_hist(pg, np, ring_h);
+        free(pg);
+    }
     pthread_barrier_init(&B.start, NULL, (unsigned)B.threads + 1);
     pthread_t *th = (pthread_t *)calloc((size_t)B.threads, sizeof *th);
     for (int t = 0; t < B.threads; ++t) pthread_create(&th[t], NULL, producer, (void *)(intptr_t)t);
     struct timespec t0, t1, t2;
+    long long thr0, thr_us0, thr1, thr_us1;
     pthread_barrier_wait(&B.start);
+    cg_throttle(&thr0, &thr_us0);
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (int t = 0; t < B.threads; ++t) pthread_join(th[t], NULL);
     clock_gettime(CLOCK_MONOTONIC, &t1);
     while (drain(1) > 0) {
     }
     clock_gettime(CLOCK_MONOTONIC, &t2);
+    cg_throttle(&thr1, &thr_us1);
     const double produce = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
     const double total = (double)(t2.tv_sec - t0.tv_sec) + 1e-9 * (double)(t2.tv_nsec - t0.tv_nsec);
     size_t right = 0, flagged = 0;
@@ -209,12 +388,35 @@ int main(int argc, char **argv) {
         flagged += B.result[i] == 2;
     }
     const double gib = (double)B.n * L512 / (double)(1ull << 30);
+    long src_h[MAXNODE + 1] = {0};
+    range_hist(B.src, B.distinct * (size_t)L512, 65536, src_h);
     printf("{\"mode\": \"%s\", \"producers\": %d, \"chunks\": %zu, \"batch\": %zu, \"pieces\": %d, "
            "\"seconds\": %.4f, \"produce_seconds\": %.4f, \"GiBps\": %.2f, \"flagged\": %zu, "
-           "\"results_correct\": %s, \"errors\": %d, \"ring_mem\": \"%s\"}\n",
+           "\"results_correct\": %s, \"errors\": %d, \"ring_mem\": \"%s\", ",
            mode, B.threads, B.n, batch, B.pieces, total, produce, gib / total, flagged,
            right == B.n && !B.errors ? "true" : "false", B.errors,
            getenv("SHA1CHUNK_VQ_RING_MEM") ? getenv("SHA1CHUNK_VQ_RING_MEM") : "uncached");
+    printf("\"placement\": {\"pin\": \"%s\", \"numa_env\": \"%s\", \"gpu_bdf\": \"%s\", \"gpu_node\": %d, "
+           "\"gpu_node_cpus_allowed\": %d, \"src_first_touch\": \"%s\", \"producers\": [",
+           B.pin ? "gpu" : "none", getenv("SHA1CHUNK_NUMA") ? getenv("SHA1CHUNK_NUMA") : "default", bdf, gnode,
+           ncpu_pin, B.local_src ? "producers" : "main thread");
+    for (int t = 0; t < B.threads && t < 64; ++t)
+        printf("%s{\"cpu_start\": %d, \"node_start\": %d, \"cpu_end\": %d, \"node_end\": %d%s", t ? ", " : "",
+               B.cpu0[t], cpu_node(B.cpu0[t]), B.cpu1[t], cpu_node(B.cpu1[t]), "}");
+    printf("], ");
+    if (B.mode == 1) {
+        printf("\"submit_buffer_nodes\": [");
+        for (int t = 0; t < B.threads && t < 64; ++t) {
+            const int k = (int)(intptr_t)B.own_page[t];
+            printf("%s%d", t ? ", " : "", k < MAXNODE ? k : -1);
+        }
+        printf("], ");
+    }
+    put_hist(stdout, "ring_pages", ring_h);
+    printf(", ");
+    put_hist(stdout, "src_pages", src_h);
+    printf(", \"cgroup_nr_throttled\": %lld, \"cgroup_throttled_usec\": %lld}}\n",
+           thr0 >= 0 && thr1 >= 0 ? thr1 - thr0 : -1, thr_us0 >= 0 && thr_us1 >= 0 ? thr_us1 - thr_us0 : -1);
     sha1chunk_vq_destroy(B.q);
     return right == B.n && !B.errors ? 0 : 1;
 }
