@@ -39,6 +39,15 @@ against the reference golden shard aggregate of the N-way split.
 config-4 list (shard.weak_golden_shard), checked against that shard's golden
 aggregate; timed like `strong`.
 
+`file` (N = 1): SURVEY 8f rank 1, make-chunks on a real file -- chunks
+0..16383 of the config-3 corpus (8 GiB) written to a temp file, hashed by
+make_chunks in-process (sha1chunk_hash_fd) and by the repo's make-chunks CLI;
+all 16384 digests checked against the reference golden aggregates.
+`master_verify` (N = 1): SURVEY 8f rank 3, 1000 verify_chunk_hash GETs at
+seeded random indices of that file (packet_handler.c:434 -> chunk.c:204-217),
+master index against the per-call path; the reference chunk.c's per-call
+cost is timed in cpu_baseline.
+
 `latency_one_chunk` (N = 1): the peer's synchronous receive-side verify,
 verify_hash() (job.c:217-228) on one 512 KiB chunk through the library, in a
 child process: cold (first call, HIP start-up included) and warm, next to the
@@ -140,7 +149,9 @@ def parse():
                     help="chunks per GPU of the config-4 weak-scaling leg (SURVEY.md 8d); 0 = skip")
     ap.add_argument("--no-latency", action="store_true")
     ap.add_argument("--no-configs", action="store_true",
-                    help="skip the config 1 / 3 / 5 legs (N = 1 only)")
+                    help="skip the config 1 / 3 / 5, file and master-verify legs (N = 1 only)")
+    ap.add_argument("--file-chunks", type=int, default=16384,
+                    help="512 KiB chunks of the file / master_verify legs' temp file (0 = skip)")
     return ap.parse_args()
 
 
@@ -344,28 +355,54 @@ def main():
         result["config4_shard8"] = _shard_leg(pkg, shard, torch, golden, 8, 1, a)
         result["config4_shard2"] = _shard_leg(pkg, shard, torch, golden, 2, 1, a)
         result["strong_projection"] = _strong_projection(result)
-    if rank == 0 and world == 1 and not a.no_configs:
-        # the other BASELINE configs on this GPU, each checked against the
-        # reference's golden digests (configs 1, 3, 5; 2 and 4 are above)
-        result["config5"] = _config5_leg(pkg, torch, golden)
-        result["config3_e2e"] = _config3_leg(pkg, torch, golden)
-        result["config1"] = _config1_leg(golden)
-        result["verify_queue"] = _verify_queue_leg(result["config3_e2e"].get("pinned_h2d_GiBps"))
-    if rank == 0 and world == 1 and not a.no_latency:
-        result["latency_one_chunk"] = _latency_one_chunk(dev)
-    if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        from oracle import oracle as O  # the CPU baseline leg only: the reference sha.c, timed
-        result["cpu_baseline"] = _cpu_baseline(O, n, L, golden, a.cpu_threads or None)
-        if "latency_one_chunk" in result:
-            result["latency_one_chunk"]["reference_sha_c_one_core_ms"] = \
-                result["cpu_baseline"].pop("one_chunk_ms")
-        if "config1" in result:
-            ref = _reference_cli(golden)
-            result["cpu_baseline"]["config1_reference_cli"] = ref
-            c1 = result["config1"]
-            c1["reference_cli_median_ms"] = ref["median_ms"]
-            for k in ("default", "device", "host_small"):
-                c1[k]["vs_reference"] = round(c1[k]["median_ms"] / ref["median_ms"], 3)
+    fpath = None
+    try:
+        if rank == 0 and world == 1 and not a.no_configs:
+            # the other BASELINE configs on this GPU, each checked against the
+            # reference's golden digests (configs 1, 3, 5; 2 and 4 are above)
+            result["config5"] = _config5_leg(pkg, torch, golden)
+            result["config3_e2e"] = _config3_leg(pkg, torch, golden)
+            result["config1"] = _config1_leg(golden)
+            result["verify_queue"] = _verify_queue_leg(result["config3_e2e"].get("pinned_h2d_GiBps"))
+            if a.file_chunks > 0:
+                fpath = _write_corpus_file(pkg, torch, a.file_chunks)
+                result["file"], fdig = _file_leg(pkg, fpath, golden, result["config3_e2e"].get("pinned_h2d_GiBps"))
+                result["master_verify"], reqs = _master_verify_leg(fpath, fdig)
+        if rank == 0 and world == 1 and not a.no_latency:
+            result["latency_one_chunk"] = _latency_one_chunk(dev)
+        if rank == 0 and world == 1 and not a.no_cpu_baseline:
+            from oracle import oracle as O  # the CPU baseline leg only: the reference sha.c, timed
+            result["cpu_baseline"] = _cpu_baseline(O, n, L, golden, a.cpu_threads or None)
+            if "latency_one_chunk" in result:
+                result["latency_one_chunk"]["reference_sha_c_one_core_ms"] = \
+                    result["cpu_baseline"].pop("one_chunk_ms")
+            if "config1" in result:
+                ref = _reference_cli(golden)
+                result["cpu_baseline"]["config1_reference_cli"] = ref
+                c1 = result["config1"]
+                c1["reference_cli_median_ms"] = ref["median_ms"]
+                for k in ("default", "device", "host_small"):
+                    c1[k]["vs_reference"] = round(c1[k]["median_ms"] / ref["median_ms"], 3)
+            if fpath and "master_verify" in result:
+                ref = _reference_master_verify(fpath, reqs)
+                result["cpu_baseline"]["master_verify_reference"] = ref
+                mv = result["master_verify"]
+                for k in ("O0", "O2"):
+                    if ref.get(k, {}).get("rest_median_ms"):
+                        mv[f"reference_{k}_per_get_ms"] = ref[k]["rest_median_ms"]
+                if ref.get("O0", {}).get("rest_median_ms") and mv.get("index", {}).get("rest_median_ms"):
+                    mv["index_speedup_vs_reference_O0"] = round(
+                        ref["O0"]["rest_median_ms"] / mv["index"]["rest_median_ms"], 1)
+            if fpath and "file" in result:
+                ref = _reference_file_cli(fpath)
+                result["cpu_baseline"]["file_reference_cli"] = ref
+                if ref.get("GiBps"):
+                    fl = result["file"]
+                    fl["reference_cli_GiBps"] = ref["GiBps"]
+                    fl["cli_vs_reference"] = round(fl["cli"]["GiBps"] / ref["GiBps"], 1)
+    finally:
+        if fpath:
+            os.unlink(fpath)
     if use_pg:
         result["config"]["control_plane"] = f"torch.distributed {backend}, world {world}"
     if rank == 0:
@@ -813,41 +850,261 @@ def _config3_leg(pkg, torch, golden, reps: int = 2) -> dict:
             "parity_ref": "digest-of-digests == golden config3.agg (reference sha.c)"}
 
 
-def _verify_queue_leg(h2d_gibps) -> dict:
+def _verify_queue_leg(h2d_gibps, runs: int = 3) -> dict:
     """SURVEY 8(f) rank 2, the received-chunk verify queue (reliable_udp.c:121
     session buffer, filled at :339; packet_handler.c:472 -> job.c:217-228):
     16384 x 512 KiB host chunks, reassembled by 4 receive threads in 1484-byte
     DATA payloads, 20 % corrupted in place before the verify, through
     tools/vq_zc_bench (C, linked against libsha1chunk.so): zero-copy
     (sha1chunk_vq_reserve / commit / release) and the reference's own call
-    shape (fill a malloc'd session buffer, sha1chunk_vq_submit).  Every result
-    is checked against the verdict the reference golden digests give
+    shape (fill a malloc'd session buffer, sha1chunk_vq_submit).  The receive
+    threads run on the GPU's NUMA node (--pin gpu: a NIC-local receive path;
+    the library's helper threads are placed there by default, SHA1CHUNK_NUMA)
+    and every run records where its threads and pages were and the cgroup's
+    CPU throttling.  `runs` runs per mode, interleaved: the median is the
+    reported GiB/s, min and max beside it.  Every result is checked against
+    the verdict the reference golden digests give
     (tests/golden/synth_4096x512k.bin); GiB/s next to this run's pinned H2D."""
     import subprocess
     tool = os.path.join(ROOT, "tools", "vq_zc_bench")
     out = {"workload": "16384 x 524288 B host chunks, 4 receive threads filling 1484-byte pieces, "
-                       "20 % corrupted, persistent drain", "pinned_h2d_GiBps": h2d_gibps}
+                       "20 % corrupted, persistent drain", "pinned_h2d_GiBps": h2d_gibps, "runs_per_mode": runs}
     if not os.path.exists(tool):
         out["error"] = "tools/vq_zc_bench not built (make -C congestion-control-with-bittorren_amd tools)"
         return out
-    for mode in ("reserve", "submit"):
-        try:
-            r = subprocess.run([tool, "--mode", mode, "--chunks", "16384", "--producers", "4",
-                                "--distinct", "4096", "--pieces", "1",
-                                "--golden", os.path.join(ROOT, "tests/golden/synth_4096x512k.bin")],
-                               capture_output=True, text=True, timeout=180, cwd=ROOT)
-            line = [x for x in r.stdout.splitlines() if x.startswith("{")]
-            rec = json.loads(line[-1]) if line else {"error": (r.stderr or r.stdout)[-300:]}
-        except Exception as e:  # a failed leg must not cost the bench line
-            rec = {"error": repr(e)[:300]}
-        if "GiBps" in rec:
-            rec["parity"] = bool(rec.get("results_correct")) and rec.get("flagged") == len(range(2, 16384, 5))
-            if h2d_gibps:
-                rec["over_h2d"] = round(rec["GiBps"] / h2d_gibps, 4)
-        out["zero_copy" if mode == "reserve" else "submit"] = rec
+    recs = {"reserve": [], "submit": []}
+    for _ in range(runs):
+        for mode in ("reserve", "submit"):
+            try:
+                r = subprocess.run([tool, "--mode", mode, "--chunks", "16384", "--producers", "4",
+                                    "--distinct", "4096", "--pieces", "1", "--pin", "gpu",
+                                    "--golden", os.path.join(ROOT, "tests/golden/synth_4096x512k.bin")],
+                                   capture_output=True, text=True, timeout=180, cwd=ROOT)
+                line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+                rec = json.loads(line[-1]) if line else {"error": (r.stderr or r.stdout)[-300:]}
+            except Exception as e:  # a failed run must not cost the bench line
+                rec = {"error": repr(e)[:300]}
+            recs[mode].append(rec)
+    for mode, key in (("reserve", "zero_copy"), ("submit", "submit")):
+        rs = recs[mode]
+        good = [r for r in rs if "GiBps" in r]
+        if not good:
+            out[key] = {"error": rs[-1].get("error") if rs else "no run"}
+            continue
+        rates = [r["GiBps"] for r in good]
+        med = good[int(np.argsort(rates)[len(rates) // 2])]
+        rec = dict(med)
+        rec["GiBps"] = float(np.median(rates))
+        rec["GiBps_runs"] = rates
+        rec["GiBps_min"], rec["GiBps_max"] = min(rates), max(rates)
+        rec["spread"] = round((max(rates) - min(rates)) / rec["GiBps"], 4)
+        rec["produce_seconds_runs"] = [r["produce_seconds"] for r in good]
+        rec["placement_runs"] = [{"producer_nodes": sorted({p["node_end"] for p in r["placement"]["producers"]}),
+                                  "cgroup_nr_throttled": r["placement"]["cgroup_nr_throttled"]} for r in good]
+        rec["parity"] = len(good) == len(rs) and all(
+            bool(r.get("results_correct")) and r.get("flagged") == len(range(2, 16384, 5)) for r in good)
+        if h2d_gibps:
+            rec["over_h2d"] = round(rec["GiBps"] / h2d_gibps, 4)
+        out[key] = rec
     out["parity"] = all(out.get(k, {}).get("parity", False) for k in ("zero_copy", "submit"))
     out["parity_ref"] = "every chunk's 0/1 == (its bytes hash to the reference golden digest); 3277 flagged"
     return out
+
+
+def _write_corpus_file(pkg, torch, chunks: int) -> str:
+    """Chunks 0..chunks-1 of the synthetic corpus (config 3's first chunks),
+    generated on the device, written to a temp file ($TMPDIR)."""
+    import tempfile
+    fd, path = tempfile.mkstemp(prefix="sha1bench_file_", suffix=".dat")
+    piece = 1024
+    tmp = torch.empty(piece * CHUNK_LEN, dtype=torch.uint8, device="cuda")
+    host = torch.empty(piece * CHUNK_LEN, dtype=torch.uint8, pin_memory=True)
+    try:
+        with os.fdopen(fd, "wb", buffering=0) as f:
+            for c0 in range(0, chunks, piece):
+                k = min(piece, chunks - c0)
+                pkg.synth_fill_device(tmp, c0, k, CHUNK_LEN)
+                host[:k * CHUNK_LEN].copy_(tmp[:k * CHUNK_LEN])
+                torch.cuda.synchronize()
+                f.write(memoryview(host.numpy())[:k * CHUNK_LEN])
+    except BaseException:
+        os.unlink(path)
+        raise
+    del tmp, host
+    torch.cuda.empty_cache()
+    return path
+
+
+def _file_leg(pkg, path: str, golden, h2d_gibps, reps: int = 3):
+    """make-chunks on a real file (make_chunks.c:14-62 ->
+    chunk.c:15-27), the file in the page cache: make_chunks in-process
+    (sha1chunk_hash_fd: parallel pread into pinned slots -> H2D -> kernel ->
+    D2H) and the repo's make-chunks CLI as a whole process, median of `reps`
+    after one warm call each; the file's page-cache read rate beside them.
+    Parity: every 4096-chunk block's digest-of-digests against the reference
+    golden weak4096 aggregates (all chunks), the golden config-3 samples in
+    range, and the CLI's "%d %s" lines against the in-process digests."""
+    import subprocess
+    size = os.path.getsize(path)
+    n = (size + CHUNK_LEN - 1) // CHUNK_LEN
+    buf = bytearray(64 << 20)
+    mv = memoryview(buf)
+    t0 = time.perf_counter()
+    with open(path, "rb", buffering=0) as f:
+        while f.readinto(mv):
+            pass
+    read_gibs = size / (time.perf_counter() - t0) / 2**30
+    pkg.make_chunks(path)  # warm: device, pinned slots
+    ts, digs = [], None
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        digs = pkg.make_chunks(path)
+        ts.append(time.perf_counter() - t0)
+    d = np.frombuffer(b"".join(digs), np.uint8).reshape(-1, 20)
+    cli = os.path.join(ROOT, "congestion-control-with-bittorren_amd", "make-chunks")
+    env = _env_without_knob()
+    cts, out = [], ""
+    for _ in range(reps + 1):
+        t0 = time.perf_counter()
+        r = subprocess.run([cli, path], capture_output=True, text=True, env=env, timeout=300)
+        cts.append(time.perf_counter() - t0)
+        if r.returncode != 0:
+            raise RuntimeError(f"make-chunks rc {r.returncode}: {r.stderr[-300:]}")
+        out = r.stdout
+    lines = out.splitlines()
+    cli_ok = lines == [f"{i} {d[i].tobytes().hex()}" for i in range(n)]
+    blocks = [hashlib.sha1(d[b * 4096:(b + 1) * 4096].tobytes()).hexdigest() == golden["weak4096"][b]
+              for b in range(n // 4096) if b < len(golden["weak4096"])]
+    samples = {int(k): v for k, v in golden["config3"]["sample"].items() if int(k) < n}
+    samp_ok = all(d[k].tobytes().hex() == v for k, v in samples.items())
+    whole = n % 4096 == 0 and len(blocks) == n // 4096
+    parity = bool(len(d) == n and cli_ok and all(blocks) and samp_ok and whole)
+    sec, csec = float(np.median(ts)), float(np.median(cts[1:]))
+    return ({"workload": f"make-chunks on a {size} B file ({n} x 512 KiB: chunks 0..{n - 1} of the config-3 "
+                         "corpus) in the page cache",
+             "chunks": n, "bytes": size,
+             "in_process": {"path": "make_chunks -> sha1chunk_hash_fd (pread ring -> H2D -> kernel -> D2H)",
+                            "seconds": round(sec, 4), "runs_s": [round(t, 4) for t in ts],
+                            "GiBps": round(size / sec / 2**30, 2)},
+             "cli": {"path": "make-chunks <file> (whole process: start, HIP init, hash, 16384 output lines)",
+                     "seconds": round(csec, 4), "first_s": round(cts[0], 4),
+                     "runs_s": [round(t, 4) for t in cts[1:]], "GiBps": round(size / csec / 2**30, 2)},
+             "page_cache_read_GiBps": round(read_gibs, 2), "pinned_h2d_GiBps": h2d_gibps,
+             "parity": parity,
+             "parity_ref": f"digest-of-digests of each 4096-chunk block == golden weak4096[b] ({len(blocks)} "
+                           f"blocks, all {n} digests; reference sha.c), {len(samples)} golden config3 samples, "
+                           "CLI lines == in-process digests"},
+            d)
+
+
+def _master_verify_leg(path: str, digests, requests: int = 1000, seed: int = 6):
+    """the sender's verify on GET (packet_handler.c:434 ->
+    chunk.c:204-217 verify_chunk_hash: re-read and re-hash 512 KiB of the
+    master file per request), `requests` GETs at seeded random indices of
+    the file through tools/master_verify_bench (C, linked against
+    libsha1chunk.so), one FILE* kept open, each call timed: the master index
+    (default: the second verify against a file builds a digest table in one
+    streamed device pass, later GETs are lookups) and the per-call path
+    (SHA1CHUNK_MASTER_INDEX=0: read + host hash per GET, the default routing
+    of one message).  verify_chunk_hash exits(-1) on a mismatch, so a
+    finished run verified every GET against the expected digests (the file
+    leg's, golden-checked); a run with wrong digests must exit 255."""
+    import subprocess
+    import tempfile
+    tool = os.path.join(ROOT, "tools", "master_verify_bench")
+    if not os.path.exists(tool):
+        return {"error": "tools/master_verify_bench not built (make -C congestion-control-with-bittorren_amd "
+                         "tools)"}, None
+    n = len(digests)
+    idx = np.random.default_rng(seed).integers(0, n, requests)
+    reqs = [(int(i), digests[int(i)].tobytes().hex()) for i in idx]
+    # the master index serves a file only once its last change is older than
+    # SHA1CHUNK_MASTER_SETTLE_MS (default 2 s, chunk.c rewrite guard)
+    age = time.time() - os.stat(path).st_ctime
+    if age < 2.2:
+        time.sleep(2.2 - age)
+    out = {"workload": f"{requests} verify_chunk_hash GETs at seeded random indices of the {n}-chunk file, "
+                       "one FILE* (a send session's master file, reliable_udp.c:180)",
+           "requests": requests}
+    with tempfile.TemporaryDirectory() as td:
+        rq = os.path.join(td, "req.txt")
+        with open(rq, "w") as f:
+            f.writelines(f"{i} {h}\n" for i, h in reqs)
+        for name, extra in (("index", {}), ("per_call", {"SHA1CHUNK_MASTER_INDEX": "0"})):
+            js = os.path.join(td, f"{name}.json")
+            r = subprocess.run([tool, path, rq, js], capture_output=True, text=True,
+                               env=_env_without_knob(extra), timeout=300)
+            if r.returncode != 0 or not os.path.exists(js):
+                out[name] = {"error": f"rc {r.returncode}: {r.stderr[-300:]}"}
+                continue
+            out[name] = json.load(open(js))
+        out["index"]["path"] = "second GET builds the file's digest table (one streamed device pass); later " \
+                               "GETs are lookups"
+        out["per_call"]["path"] = "SHA1CHUNK_MASTER_INDEX=0: fseek + fread 512 KiB + shahash on the host per GET"
+        bad = os.path.join(td, "bad.txt")
+        with open(bad, "w") as f:
+            f.writelines(f"{reqs[0][0]} {'0' * 40}\n" for _ in range(3))
+        r = subprocess.run([tool, path, bad, os.path.join(td, "bad.json")], capture_output=True, text=True,
+                           env=_env_without_knob(), timeout=120)
+        out["mismatch_exits"] = r.returncode == 255 and "Unmatched chunk hashes" in r.stderr
+    i, p = out.get("index", {}), out.get("per_call", {})
+    if i.get("rest_median_ms") and p.get("rest_median_ms"):
+        out["index_speedup_vs_per_call"] = round(p["rest_median_ms"] / i["rest_median_ms"], 1)
+    out["parity"] = bool(i.get("verified") == requests and p.get("verified") == requests and out["mismatch_exits"])
+    out["parity_ref"] = "every GET verified by verify_chunk_hash itself (exit(-1) on mismatch) against the file " \
+                        "leg's golden-checked digests; wrong digests exit 255"
+    return out, reqs
+
+
+def _reference_master_verify(path: str, reqs, requests: int = 200) -> dict:
+    """The reference chunk.c's verify_chunk_hash (+ sha.c, utility.c,
+    packet.c; our timing main, tools/master_verify_bench.c) built from its
+    sources into oracle/_ref with its Makefile's flags and at -O2, `requests`
+    GETs each.  Indices below 8192 only: the reference seeks through a
+    uint32_t offset (chunk.c:193), which wraps past 4 GiB."""
+    import subprocess
+    import tempfile
+    sub = [(i, h) for i, h in reqs if i < 8192][:requests]
+    out = {"requests": len(sub), "note": "indices < 8192 (chunk.c:193 seeks via a uint32_t offset)"}
+    with tempfile.TemporaryDirectory() as td:
+        rq = os.path.join(td, "req.txt")
+        with open(rq, "w") as f:
+            f.writelines(f"{i} {h}\n" for i, h in sub)
+        for k, exe in (("O0", "master_verify_ref"), ("O2", "master_verify_ref_O2")):
+            tool = os.path.join(ROOT, "oracle", "_ref", exe)
+            js = os.path.join(td, f"{k}.json")
+            if not os.path.exists(tool):
+                out[k] = {"error": f"oracle/_ref/{exe} not built"}
+                continue
+            r = subprocess.run([tool, path, rq, js], capture_output=True, text=True, timeout=300)
+            out[k] = json.load(open(js)) if r.returncode == 0 and os.path.exists(js) else \
+                {"error": f"rc {r.returncode}: {r.stderr[-200:]}"}
+    out["O0"]["build"] = "reference Makefile flags (-g, no -O)"
+    out["O2"]["build"] = "-O2"
+    return out
+
+
+def _reference_file_cli(path: str, chunks: int = 1024) -> dict:
+    """The reference's own make-chunks (oracle/_ref, its Makefile's flags) on
+    the first `chunks` chunks of the file leg's file (a bounded sample: the
+    whole 8 GiB would take ~25 s at -O0)."""
+    import subprocess
+    import tempfile
+    fd, sp = tempfile.mkstemp(prefix="sha1bench_ref_", suffix=".dat")
+    try:
+        with os.fdopen(fd, "wb") as o, open(path, "rb") as f:
+            o.write(f.read(chunks * CHUNK_LEN))
+        exe = os.path.join(ROOT, "oracle", "_ref", "make-chunks")
+        t0 = time.perf_counter()
+        r = subprocess.run([exe, sp], capture_output=True, text=True, timeout=300)
+        sec = time.perf_counter() - t0
+        if r.returncode != 0:
+            return {"error": f"rc {r.returncode}"}
+        return {"sample": f"first {chunks} chunks ({chunks * CHUNK_LEN} B) of the file leg's file",
+                "seconds": round(sec, 3), "GiBps": round(chunks * CHUNK_LEN / sec / 2**30, 3),
+                "lines": len(r.stdout.splitlines())}
+    finally:
+        os.unlink(sp)
 
 
 def _env_without_knob(extra=None) -> dict:

@@ -12,6 +12,8 @@
 #include <cstring>
 #include <functional>
 #include <mutex>
+#include <pthread.h>
+#include <sched.h>
 #include <thread>
 #include <vector>
 
@@ -27,7 +29,14 @@ inline void cpu_relax() { __builtin_ia32_pause(); }
 // not pay a thread start or a futex wake-up.
 class PartPool {
 public:
-    explicit PartPool(int helpers) {
+    // cpus (optional): the helpers run on these host CPUs only -- the ones
+    // near the GPU whose pinned buffers they fill (sha1_runtime.hip
+    // near_cpus); the calling thread's own placement is the caller's
+    explicit PartPool(int helpers, const cpu_set_t* cpus = nullptr) {
+        if (cpus) {
+            cpus_ = *cpus;
+            pin_ = true;
+        }
         for (int i = 0; i < helpers; ++i) th_.emplace_back([this] { loop(); });
     }
     ~PartPool() {
@@ -86,6 +95,7 @@ private:
         }
     }
     void loop() {
+        if (pin_) (void)pthread_setaffinity_np(pthread_self(), sizeof cpus_, &cpus_);
         uint64_t seen = 0;
         for (;;) {
             int spin = 0;
@@ -111,6 +121,8 @@ private:
         }
     }
     std::vector<std::thread> th_;
+    cpu_set_t cpus_{};
+    bool pin_ = false;
     std::mutex mu_;
     std::condition_variable cv_, done_;
     std::atomic<uint64_t> gen_{0};

@@ -40,6 +40,66 @@
 
 namespace {
 using s1host::PartPool;
+
+// Host CPUs near HIP device `id`: the CPUs of its NUMA node (the numa_node
+// of its PCI device) within this process's affinity mask.  The library's
+// helper threads -- the verify queue's copies into the pinned ring, the
+// pageable-batch packing, the file pipeline's preads into pinned slots --
+// run there, beside the pinned memory they write (hipHostMalloc already
+// places it on the GPU's node: profiles/vq_place_r06*.jsonl) and the GPU that
+// reads it.  SHA1CHUNK_NUMA=off (or 0) leaves them to the scheduler.
+// nullptr: no placement (off, one node, node unknown, or none of its CPUs
+// allowed).
+const cpu_set_t* near_cpus(int id) {
+    struct Near {
+        std::once_flag once;
+        bool ok = false;
+        cpu_set_t set;
+    };
+    static Near near[64];
+    if (id < 0 || id >= 64) return nullptr;
+    Near& n = near[id];
+    std::call_once(n.once, [&] {
+        const char* e = getenv("SHA1CHUNK_NUMA");
+        if (e && (!strcmp(e, "off") || !strcmp(e, "0"))) return;
+        char bdf[64] = {0};
+        if (hipDeviceGetPCIBusId(bdf, sizeof bdf, id) != hipSuccess) {
+            (void)hipGetLastError();
+            return;
+        }
+        for (char* c = bdf; *c; ++c) *c = static_cast<char>(tolower(static_cast<unsigned char>(*c)));
+        int node = -1;
+        char path[160];
+        snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bdf);
+        if (FILE* f = fopen(path, "r")) {
+            if (fscanf(f, "%d", &node) != 1) node = -1;
+            fclose(f);
+        }
+        if (node < 0) return;
+        char list[4096] = {0};
+        snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+        if (FILE* f = fopen(path, "r")) {
+            if (!fgets(list, sizeof list, f)) list[0] = 0;
+            fclose(f);
+        }
+        cpu_set_t allowed, mine;
+        if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return;
+        CPU_ZERO(&mine);
+        for (char* save = nullptr, *tok = strtok_r(list, ",\n", &save); tok; tok = strtok_r(nullptr, ",\n", &save)) {
+            int a = 0, b = 0;
+            const int k = sscanf(tok, "%d-%d", &a, &b);
+            if (k < 1) continue;
+            if (k == 1) b = a;
+            for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
+                if (CPU_ISSET(c, &allowed)) CPU_SET(c, &mine);
+        }
+        // nothing to gain when every allowed CPU is on this node already
+        if (CPU_COUNT(&mine) == 0 || CPU_EQUAL(&mine, &allowed)) return;
+        n.set = mine;
+        n.ok = true;
+    });
+    return n.ok ? &n.set : nullptr;
+}
 using s1host::pool_copy;
 thread_local std::string t_err;
 thread_local int t_dev = 0;
@@ -498,7 +558,7 @@ int stage_and_launch(Device& D, Slot& s, const uint8_t* base, const uint64_t* of
     } else {
         // pack in runs of ~64 MiB and start each run's H2D as soon as it is
         // packed, so the copy engine works while the rest is packed
-        if (!D.pack) D.pack.reset(new PartPool(pack_threads() - 1));
+        if (!D.pack) D.pack.reset(new PartPool(pack_threads() - 1, near_cpus(D.id)));
         static const size_t piece = [] {  // SHA1CHUNK_PACK_PIECE_MIB, 0 = whole slot
             const char* e = getenv("SHA1CHUNK_PACK_PIECE_MIB");
             const size_t mib = e ? static_cast<size_t>(std::max(0, atoi(e))) : 64;
@@ -1017,7 +1077,7 @@ long hash_file_devices(int fd, off_t pos, off_t end, int nd, int read_threads, F
             const uint64_t c0 = chunks * g / nd, c1 = chunks * (g + 1) / nd;
             const off_t a = pos + static_cast<off_t>(c0 * L);
             const off_t b = std::min(end, pos + static_cast<off_t>(c1 * L));
-            PartPool pool(std::max(1, read_threads) - 1);
+            PartPool pool(std::max(1, read_threads) - 1, near_cpus(g_dev[t_dev].id));
             ParFile f{fd, a, b, &pool};
             struct Shift {
                 FdSink* sk;
@@ -1063,7 +1123,7 @@ long s1be_hash_fd(int fd, uint8_t* digests, size_t max_chunks, size_t* total_chu
         if (nd > 1) {
             n = hash_file_devices(fd, pos, end, nd, read_threads, &sk);
         } else {
-            PartPool pool(read_threads - 1);
+            PartPool pool(read_threads - 1, near_cpus(g_dev[t_dev].id));
             ParFile f{fd, pos, end, &pool};
             n = hash_stream_sized(par_reader, &f, fd_sink, &sk, static_cast<uint64_t>(f.end - f.pos));
             (void)lseek(fd, f.pos, SEEK_SET);
@@ -1677,6 +1737,12 @@ int pvq_publish(Pvq* P);
 // wait that only the caller can end -- the oldest region of the data ring
 // is a reserved buffer not yet committed, or collected and not released --
 // fails at once when `stuck` says so.
+// Bound on any one wait (SHA1CHUNK_VQ_WAIT_S, default 120 s).
+std::chrono::seconds pvq_wait_bound() {
+    static const std::chrono::seconds b(std::max<uint64_t>(1, env_u64("SHA1CHUNK_VQ_WAIT_S", 120)));
+    return b;
+}
+
 template <typename Pred, typename Stuck>
 int pvq_wait(Pvq* P, Pred pred, const char* what, Stuck stuck) {
     const auto t0 = std::chrono::steady_clock::now();
@@ -1685,13 +1751,11 @@ int pvq_wait(Pvq* P, Pred pred, const char* what, Stuck stuck) {
         if ((rc = pvq_reap(P))) return rc;
         if (pred()) return SHA1CHUNK_OK;
         if (P->open_count && (rc = pvq_publish(P))) return rc;
-        if (stuck())
-            return fail(SHA1CHUNK_ENOMEM,
-                        "vq: %s: the ring's oldest region is this thread's own reserved buffer, not committed "
-                        "or not released (%zu reserved buffers held)",
-                        what, P->held.size());
+        if (const char* why = stuck())
+            return fail(SHA1CHUNK_ENOMEM, "vq: %s: the ring's oldest region is %s (%zu reserved buffers held)", what,
+                        why, P->held.size());
         if (P->inflight && (rc = pvq_ensure_drain(P))) return rc;
-        if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(120))
+        if (std::chrono::steady_clock::now() - t0 > pvq_wait_bound())
             return fail(SHA1CHUNK_EHIP, "vq: %s timed out (drain not progressing)", what);
         ++P->n_sleeps;
         // sleep without the queue's lock: the other threads' commits, polls
@@ -1706,7 +1770,7 @@ int pvq_wait(Pvq* P, Pred pred, const char* what, Stuck stuck) {
 }
 template <typename Pred>
 int pvq_wait(Pvq* P, Pred pred, const char* what) {
-    return pvq_wait(P, pred, what, [] { return false; });
+    return pvq_wait(P, pred, what, [] { return static_cast<const char*>(nullptr); });
 }
 
 // Queues alive at process exit (a caller that never destroys its queue):
@@ -1960,7 +2024,7 @@ Pvq* pvq_create(Device* D, size_t batch, uint32_t max_chunk_len, int cus) {
         pvq_destroy(P);
         return nullptr;
     }
-    P->copier = new PartPool(vq_copy_helpers());
+    P->copier = new PartPool(vq_copy_helpers(), near_cpus(P->dev));
     pvq_track(P, true);
     return P;
 }
@@ -1980,22 +2044,45 @@ void pvq_stop_all_at_exit() {
 
 // Room for `len` bytes in the data ring (a region never wraps it): a bounded
 // wait while in-flight groups can free space.  Returns the new region's id.
+constexpr auto kHeldResultWait = std::chrono::milliseconds(2);
 int pvq_alloc(Pvq* P, uint32_t len, bool reserved, uint64_t* id) {
     const uint64_t need = round_up(std::max<uint32_t>(len, 1), kAlign);
     auto pos = [&] {
         const uint64_t t = P->byte_tail;
         return (t % P->nbytes) + need > P->nbytes ? t + (P->nbytes - t % P->nbytes) : t;
     };
-    // Only the caller's own buffer at the ring's head makes the wait hopeless
-    // (this thread cannot commit or release it while it waits here); another
-    // thread's reservation there is a session still filling or not yet
-    // released, which that thread will commit or release, so the
-    // call waits for it as for any in-flight group (bounded, pvq_wait).
+    // The wait is hopeless when the ring's head is
+    //  * the caller's own reservation, not committed (this thread cannot
+    //    commit it while it waits here), or
+    //  * a reserved buffer whose result is finished but that is not released,
+    //    whoever holds it: only a poll() that hands out the result and the
+    //    release() after it free that room.  When every receive thread sits in
+    //    reserve() nobody polls, so after a short grace (another thread may be
+    //    polling and releasing right now) the call fails and its caller polls
+    //    and releases (round 6: four receive threads all waiting here stalled
+    //    for the whole 120 s bound).
+    // Another thread's reservation not yet committed is a session still
+    // filling, which that thread will commit: the call waits for
+    // it as for any in-flight group (bounded, pvq_wait).
     const std::thread::id me = std::this_thread::get_id();
-    auto stuck = [&] {
-        if (P->regions.empty()) return false;
+    std::chrono::steady_clock::time_point held_since{};
+    bool held_seen = false;
+    auto stuck = [&]() -> const char* {
+        if (P->regions.empty()) return nullptr;
         const PvqRegion& r = P->regions.front();
-        return r.reserved && !r.released && (!r.committed || r.collected) && r.owner == me;
+        if (!r.reserved || r.released) return nullptr;
+        const char* own = "this thread's own reserved buffer, not committed or not released";
+        if (!r.committed) return r.owner == me ? own : nullptr;
+        if (!r.collected) return nullptr;
+        if (r.owner == me) return own;
+        const auto now = std::chrono::steady_clock::now();
+        if (!held_seen) {
+            held_seen = true;
+            held_since = now;
+        }
+        return now - held_since >= kHeldResultWait
+                   ? "a verified buffer whose result is not yet polled and released (poll() and release() free it)"
+                   : nullptr;
     };
     if (int rc = pvq_wait(P, [&] { return pos() + need - P->byte_head <= P->nbytes; }, "data ring full", stuck))
         return rc;
@@ -2233,7 +2320,7 @@ void* s1be_vq_create(size_t batch, uint32_t max_chunk_len) {
     q->maxlen = max_chunk_len;
     q->stride = round_up(max_chunk_len, kAlign);
     q->meta = round_up(q->cap * (8 + 4 + 20), kAlign);
-    q->copier = new PartPool(vq_copy_helpers());
+    q->copier = new PartPool(vq_copy_helpers(), near_cpus(D->id));
     const size_t hbytes = q->meta + q->cap * q->stride;
     for (auto& S : q->set) {
         if (S.h.ensure(hbytes) || S.d.ensure(hbytes + q->cap * 21) || S.res.ensure(q->cap) ||

@@ -208,6 +208,52 @@ def test_another_threads_reservation_makes_submit_wait(pkg, dev, monkeypatch):
         assert got == want
 
 
+def test_other_threads_finished_unreleased_head_fails_fast(pkg, dev, monkeypatch):
+    """Round 6: four receive threads all waiting in reserve() while the
+    ring's head held another session's verified but unpolled buffer stalled
+    for the whole 120 s bound -- nobody polled.  A session thread reserves,
+    fills and commits a ring's worth of buffers and polls nothing; once their
+    results are in, the main thread's reserve fails with ENOMEM within
+    seconds (the grace is 2 ms) and names the fix; after a poll and the
+    releases it succeeds."""
+    monkeypatch.setenv("SHA1CHUNK_VQ_MODE", "persistent")
+    monkeypatch.setenv("SHA1CHUNK_VQ_RING_MIB", "8")  # 128 chunks of 64 KiB
+    chunk = np.frombuffer(bytes(range(256)) * 256, np.uint8)
+    dig = hashlib.sha1(chunk.tobytes()).digest()
+    with pkg.VerifyQueue(batch=64, max_chunk_len=65536) as q:
+        held, errors = [], []
+
+        def session():
+            try:
+                for i in range(128):
+                    r = q.reserve(65536)
+                    r.view[:] = chunk
+                    q.commit(r, dig, i)
+                    held.append(r)
+            except Exception as e:
+                errors.append(repr(e))
+
+        t = threading.Thread(target=session)
+        t.start()
+        t.join(timeout=60)
+        assert not errors and len(held) == 128, errors
+        time.sleep(0.5)  # the drain finishes the 128 chunks (two groups)
+        t0 = time.time()
+        with pytest.raises(pkg.Sha1ChunkError) as ei:
+            q.reserve(65536)
+        assert time.time() - t0 < 5.0
+        assert ei.value.code == pkg.sha1chunk.ENOMEM and "not yet polled and released" in str(ei.value)
+        got = dict(q.poll(wait=True, max_results=256))
+        assert got == {i: 0 for i in range(128)}
+        for r in held:
+            q.release(r)
+        r = q.reserve(65536)
+        r.view[:] = chunk
+        q.commit(r, dig, 500)
+        assert q.poll(wait=True) == [(500, 0)]
+        q.release(r)
+
+
 def test_queue_create_destroy_beside_a_busy_queue(pkg, dev, corpus, monkeypatch):
     """creating and destroying a queue must not wait for the
     whole device.  One thread keeps a persistent queue continuously busy for
@@ -333,9 +379,12 @@ def _config2_on_fresh_stream(pkg, dev):
 
 def test_wait_behind_busy_drains_is_bounded(pkg, dev, corpus, monkeypatch):
     """a config-2 batch launched on a fresh stream while
-    four verify queues are continuously fed finishes within its solo time +
-    10 ms (the bound stated in include/sha1chunk.h): no drain holds a
-    hardware queue the batch's stream is mapped to for longer than that."""
+    four verify queues are continuously fed is not held behind their drains.
+    The regression this guards (the queues' streams at the default priority)
+    took 12-26 ms against 6 ms solo; the pass/fail check compares medians
+    with a relative margin (1.5x) so host or GIL jitter alone cannot fail it
+    (ADVICE r5); the absolute "solo + 10 ms" of include/sha1chunk.h is
+    printed, measured in the bench tooling, not asserted here."""
     import threading
     monkeypatch.setenv("SHA1CHUNK_VQ_MODE", "persistent")
     monkeypatch.setenv("SHA1CHUNK_VQ_RING_MIB", "256")
@@ -348,7 +397,7 @@ def test_wait_behind_busy_drains_is_bounded(pkg, dev, corpus, monkeypatch):
     digs = [want[i].tobytes() for i in range(64)]
     old_switch = sys.getswitchinterval()
     sys.setswitchinterval(1e-4)
-    solo = min(_config2_on_fresh_stream(pkg, dev)[0] for _ in range(3))
+    solo = float(np.median([_config2_on_fresh_stream(pkg, dev)[0] for _ in range(3)]))
     stop, started = threading.Event(), threading.Barrier(5)
     errors, counts = [], [0] * 4
 
@@ -390,4 +439,5 @@ def test_wait_behind_busy_drains_is_bounded(pkg, dev, corpus, monkeypatch):
     assert all(c > 0 for c in counts), counts
     print(f"config-2 batch on a fresh stream: solo {solo * 1e3:.2f} ms, beside 4 fed queues "
           f"{', '.join(f'{b * 1e3:.2f}' for b in busy)} ms")
-    assert max(busy) <= solo + 0.010, (solo, busy)
+    print(f"within solo + 10 ms: {max(busy) <= solo + 0.010}")
+    assert float(np.median(busy)) <= 1.5 * solo, (solo, busy)

@@ -20,9 +20,11 @@ for r in $(seq 1 "$REPS"); do
   for numa in $NUMAS; do
     for pin in none gpu; do
       for mode in $MODES; do
-        line=$(SHA1CHUNK_NUMA=$numa timeout -k 10 120 tools/vq_zc_bench --mode "$mode" --chunks 16384 \
+        line=$(VQ_ZC_TRACE=1 SHA1CHUNK_NUMA=$numa timeout -k 10 60 tools/vq_zc_bench --mode "$mode" --chunks 16384 \
                --producers 4 --distinct 4096 --pieces 1 --pin "$pin" \
-               --golden tests/golden/synth_4096x512k.bin) || { echo "vq_zc_bench failed rc=$?" >&2; exit 1; }
+               --golden tests/golden/synth_4096x512k.bin 2>"${OUT%.jsonl}.last.err") || {
+          rc=$?; echo "vq_zc_bench failed rc=$rc (rep $r numa $numa pin $pin mode $mode)" >&2
+          cat "${OUT%.jsonl}.last.err" >&2; exit 1; }
         echo "{\"rep\": $r, \"numa\": \"$numa\", $(echo "$line" | sed 's/^{//')" >> "$OUT"
         echo "rep $r numa $numa pin $pin $mode: $(echo "$line" | python3 -c 'import json,sys; d=json.load(sys.stdin); print(d["GiBps"], d["produce_seconds"], d["placement"]["gpu_node"], d["placement"]["ring_pages"])')"
       done

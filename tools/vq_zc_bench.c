@@ -330,6 +330,7 @@ int main(int argc, char **argv) {
     B.bufp = (void **)calloc(B.n, sizeof *B.bufp);
     B.result = (volatile uint8_t *)calloc(B.n, 1);
     pthread_mutex_init(&B.err_mu, NULL);
+    if (getenv("VQ_ZC_TRACE")) fprintf(stderr, "vq_zc_bench: gpu node %d (%s), %d cpus\n", gnode, bdf, ncpu_pin);
     B.q = sha1chunk_vq_create(batch, L512);
     if (!B.q) {
         fprintf(stderr, "vq_zc_bench: vq_create: %s\n", sha1chunk_last_error());
@@ -349,6 +350,7 @@ int main(int argc, char **argv) {
         while (sha1chunk_vq_poll(B.q, tags, mis, 64, 1) > 0) {
         }
     }
+    if (getenv("VQ_ZC_TRACE")) fprintf(stderr, "vq_zc_bench: warm done\n");
     /* the data ring's pages: walk it once, one reservation after another */
     long ring_h[MAXNODE + 1] = {0};
     {
@@ -365,6 +367,7 @@ int main(int argc, char **argv) {
         page_hist(pg, np, ring_h);
         free(pg);
     }
+    if (getenv("VQ_ZC_TRACE")) fprintf(stderr, "vq_zc_bench: ring walked\n");
     pthread_barrier_init(&B.start, NULL, (unsigned)B.threads + 1);
     pthread_t *th = (pthread_t *)calloc((size_t)B.threads, sizeof *th);
     for (int t = 0; t < B.threads; ++t) pthread_create(&th[t], NULL, producer, (void *)(intptr_t)t);
@@ -375,6 +378,7 @@ int main(int argc, char **argv) {
     clock_gettime(CLOCK_MONOTONIC, &t0);
     for (int t = 0; t < B.threads; ++t) pthread_join(th[t], NULL);
     clock_gettime(CLOCK_MONOTONIC, &t1);
+    if (getenv("VQ_ZC_TRACE")) fprintf(stderr, "vq_zc_bench: producers joined\n");
     while (drain(1) > 0) {
     }
     clock_gettime(CLOCK_MONOTONIC, &t2);
