@@ -1,18 +1,21 @@
 /*
- * sha1_host.c -- the host-side SHA-1 compression behind the library's opt-in
- * small-call path (SHA1CHUNK_HOST_SMALL, sha1_runtime.hip).
+ * sha1_host.c -- the host-side SHA-1 compression behind the library's
+ * single-message path (csrc/frontend.c routing).
  *
  * One chunk per call is the peer's synchronous receive verify
  * (packet_handler.c:472 -> job.c:217-228 verify_hash -> chunk.c:168-185
  * get_chunk_hash -> chunk.c:35-51 shahash).  On the GPU that is one lane's
  * serial chain of 8193 compressions, 6.0 ms for 512 KiB; the reference's
- * sha.c does it in ~0.7 ms on one core.  A caller that sets
- * SHA1CHUNK_HOST_SMALL=<bytes> gets calls of at most that many bytes hashed
- * here instead ("keep the CPU path for
- * batch size 1").  It is not a fallback: the library still requires a
- * gfx950 device for every call (no device -> SHA1CHUNK_ENODEV), the knob is
- * off by default, and every batch above the threshold -- and every test,
- * smoke and bench number of the GPU path -- runs on the kernels.
+ * sha.c does it in ~0.7 ms on one core, this file in ~0.2 ms.  So by default
+ * the reference's single-message calls (shahash and what is built on it,
+ * the SHA1Update/SHA1Final trio) and make_chunks on a regular file of at
+ * most 4 MiB are hashed here ("keep a CPU path",
+ * "the streaming trio stays CPU"); SHA1CHUNK_HOST_SMALL=0 sends them to the
+ * kernels, SHA1CHUNK_HOST_SMALL=<bytes> routes by size.  It is not a
+ * fallback: the library still requires a gfx950 device for every call (no
+ * device -> SHA1CHUNK_ENODEV), and every batch, device-resident,
+ * verify-queue and larger-file call -- and every kernel parity test, smoke
+ * and bench number of the GPU path -- runs on the kernels.
  *
  * Compression (FIPS 180-4 section 6.1.2, the function sha.c:176-451
  * implements): the x86 SHA extensions when the CPU has them (sha1rnds4 does

@@ -1,5 +1,6 @@
-/* sha1_host.h -- host-side SHA-1 for the opt-in small-call path
- * (SHA1CHUNK_HOST_SMALL; sha1_host.c).  Internal to libsha1chunk.so (hidden
+/* sha1_host.h -- host-side SHA-1 for the single-message path (the default
+ * routing of shahash / the SHA1Update trio / small files, csrc/frontend.c;
+ * SHA1CHUNK_HOST_SMALL; sha1_host.c).  Internal to libsha1chunk.so (hidden
  * symbols); tests/test_host_small.py builds sha1_host.c on its own to check
  * it on the CPU. */
 #ifndef SHA1_HOST_H

@@ -165,7 +165,7 @@ __global__ __launch_bounds__(kMixedThreads) void sha1_mixed_kernel(BatchArgs A) 
 __device__ __forceinline__ uint32_t group_units(const BatchArgs& A, uint32_t group, uint32_t U) {
     const uint32_t e = group * 64u + (threadIdx.x & 63u);
     const bool valid = e < A.n;
-    Entry en = fetch_entry(A, valid ? e : min(group * 64u, A.n - 1u));
+    Entry en = fetch_entry(A, valid ? e : fallback_entry(A, group));
     const uint32_t T = valid ? total_blocks(en.len) : 0u;
     const uint32_t Tmax = __builtin_amdgcn_readfirstlane(wave_max(T));
     return (Tmax + 2u * U - 1u) / (2u * U) * 2u;
@@ -1212,3 +1212,28 @@ hipError_t launch_compare(const uint8_t* dig, const uint8_t* exp, uint32_t n, ui
                        mismatch);
     return hipGetLastError();
 }
+
+#ifdef SHA1CHUNK_CHECKED
+// Bounds violations counted by the checked build's fetch_entry on every
+// device since the last reset (reset != 0 zeroes the counters after reading).
+// Exported by the checked backend only: tests/conftest.py reads it after each
+// GPU test when SHA1CHUNK_CHECKED=1.
+extern "C" __attribute__((visibility("default"))) long long s1be_checked_violations(int reset) {
+    int cur = 0, nd = 0;
+    if (hipGetDevice(&cur) != hipSuccess || hipGetDeviceCount(&nd) != hipSuccess) return -1;
+    long long total = 0;
+    for (int d = 0; d < nd; ++d) {
+        unsigned int v = 0;
+        if (hipSetDevice(d) != hipSuccess ||
+            hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_checked_oob), sizeof v, 0, hipMemcpyDeviceToHost) != hipSuccess)
+            return -1;
+        total += v;
+        const unsigned int zero = 0;
+        if (reset && hipMemcpyToSymbol(HIP_SYMBOL(g_checked_oob), &zero, sizeof zero, 0, hipMemcpyHostToDevice) !=
+                         hipSuccess)
+            return -1;
+    }
+    (void)hipSetDevice(cur);
+    return total;
+}
+#endif

@@ -24,13 +24,49 @@ struct Entry {
     uint32_t len;
 };
 
+#ifdef SHA1CHUNK_CHECKED
+// The bounds-checked backend (`make checked`): every
+// entry index and every A.order value is checked against the batch; a
+// violation is counted here (read by s1be_checked_violations, sha1_kernels.hip),
+// the first few printed, and the index clamped so the access stays inside
+// the batch -- the run reports the bug instead of faulting the GPU.
+__device__ unsigned int g_checked_oob;
+
+__device__ __forceinline__ uint32_t checked_index(uint32_t i, uint32_t n, const char* what) {
+    if (i < n) return i;
+    if (atomicAdd(&g_checked_oob, 1u) < 8u)
+        printf("sha1chunk checked: %s %u >= n %u (block %u, thread %u)\n", what, i, n, blockIdx.x, threadIdx.x);
+    return n ? n - 1u : 0u;
+}
+#endif
+
 __device__ __forceinline__ Entry fetch_entry(const BatchArgs& A, uint32_t e) {
     Entry r;
+#ifdef SHA1CHUNK_CHECKED
+    e = checked_index(e, A.n, "entry index");
+    r.id = A.order ? checked_index(A.order[e], A.n, "A.order value") : e;
+#else
     r.id = A.order ? A.order[e] : e;
+#endif
     const uint64_t off = A.off ? A.off[r.id] : (uint64_t)r.id * A.ulen;
     r.p = A.base + off;
     r.len = A.len ? A.len[r.id] : A.ulen;
     return r;
+}
+
+// The entry a lane past the batch reads instead of its own (its loads are
+// valid and unused): the group's first chunk, or -- for a group wholly past
+// the batch (the empty second pair of a split workgroup when the group count
+// is odd) -- the batch's last entry, never group*64, which indexes past
+// A.order (round 5's fault, gpurun_out/pytest_sort16_r05.log; fixed in
+// 2705501).  SHA1CHUNK_AB_UNCLAMPED puts the unclamped index back: only for
+// the checked build's negative test (`make checked-unclamped`).
+__device__ __forceinline__ uint32_t fallback_entry(const BatchArgs& A, uint32_t group) {
+#ifdef SHA1CHUNK_AB_UNCLAMPED
+    return group * 64u;
+#else
+    return min(group * 64u, A.n - 1u);
+#endif
 }
 
 __device__ __forceinline__ void load_init(const BatchArgs& A, uint32_t id, uint32_t (&h)[5]) {
@@ -356,7 +392,7 @@ __device__ __forceinline__ void coop_sources(const BatchArgs& A, uint32_t group,
 #pragma unroll
     for (uint32_t i = 0; i < (uint32_t)LANES; ++i) {
         const uint32_t ej = group * 64u + (64u / LANES) * i + lane / LANES;
-        src[i] = reinterpret_cast<const u32x4u*>(fetch_entry(A, ej < A.n ? ej : min(group * 64u, A.n - 1u)).p) + (lane % LANES);
+        src[i] = reinterpret_cast<const u32x4u*>(fetch_entry(A, ej < A.n ? ej : fallback_entry(A, group)).p) + (lane % LANES);
     }
 }
 
@@ -740,7 +776,7 @@ __device__ __forceinline__ void split_body(const BatchArgs& A, uint8_t* lds, uin
     const uint32_t group = wg * PAIRS + (uint32_t)pair;
     const uint32_t e = group * 64u + (uint32_t)lane;
     const bool valid = e < A.n;
-    Entry en = fetch_entry(A, valid ? e : min(group * 64u, A.n - 1u));
+    Entry en = fetch_entry(A, valid ? e : fallback_entry(A, group));
     if (!valid) en.len = 0;
     // update mode (A.out_state): whole blocks only, no padding
     const uint32_t T = valid ? (A.out_state ? (en.len >> 6) : total_blocks(en.len)) : 0u;
@@ -967,7 +1003,7 @@ __device__ __forceinline__ void fused_lane_stages(const Entry& en, bool valid, u
 __device__ __forceinline__ void fused_body(const BatchArgs& A, uint32_t e) {
     const uint32_t group = e / 64u;
     const bool valid = e < A.n;
-    Entry en = fetch_entry(A, valid ? e : min(group * 64u, A.n - 1u));
+    Entry en = fetch_entry(A, valid ? e : fallback_entry(A, group));
     if (!valid) en.len = 0;
     uint32_t h[5];
     load_init(A, en.id, h);
@@ -1056,7 +1092,7 @@ __device__ __forceinline__ void glds_stage_step(const uint8_t* const (&p)[4], ui
 __device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, uint8_t* lds) {
     const uint32_t group = e / 64u, lane = e & 63u;
     const bool valid = e < A.n;
-    Entry en = fetch_entry(A, valid ? e : min(group * 64u, A.n - 1u));
+    Entry en = fetch_entry(A, valid ? e : fallback_entry(A, group));
     if (!valid) en.len = 0;
     uint32_t h[5];
     load_init(A, en.id, h);
@@ -1093,7 +1129,7 @@ __device__ __forceinline__ void fused_coop_body(const BatchArgs& A, uint32_t e, 
 #pragma unroll
         for (uint32_t i = 0; i < 4; ++i) {
             const uint32_t ej = group * 64u + 16u * i + (lane >> 2);
-            p[i] = fetch_entry(A, ej < A.n ? ej : min(group * 64u, A.n - 1u)).p + 16u * piece;
+            p[i] = fetch_entry(A, ej < A.n ? ej : fallback_entry(A, group)).p + 16u * piece;
         }
         const uint32_t base = lds_addr(lds);
         // blocks 0..3 in flight (past the bulk region: the last block again,

@@ -35,8 +35,19 @@ extern "C" {
 #endif
 
 /* Hashes every 512 KiB chunk of fp (last one at its true length) into the
- * caller-allocated chunk_hashes[i] (20 bytes each); returns the count. The
- * file is streamed through pinned host buffers and hashed in device batches. */
+ * caller-allocated chunk_hashes[i] (20 bytes each); returns the count.  A
+ * regular file of more than 4 MiB (8 chunks) -- and any stream or pipe -- is
+ * read into pinned host buffers and hashed in device batches on the gfx950
+ * kernels; a regular file of at most 4 MiB (BASELINE config 1's tmp/C.tar is
+ * 2 MiB) is hashed on the host by default, where its few serial chains take
+ * ~0.2 ms each instead of a kernel launch plus ~6 ms per chain
+ * (SHA1CHUNK_HOST_SMALL changes this: include/sha1chunk.h).
+ *
+ * shahash, get_chunk_hash, verify_hash and verify_chunk_hash hash ONE message
+ * per call; by default on the host (a gfx950 device is still required),
+ * SHA1CHUNK_HOST_SMALL=0 puts them on the kernels.  verify_chunk_hash serves
+ * a master file from a digest table built in one device pass from its second
+ * call on (SHA1CHUNK_MASTER_INDEX=0: per call). */
 int make_chunks(FILE *fp, uint8_t **chunk_hashes);
 
 void shahash(uint8_t *chr, int len, uint8_t *target);

@@ -5,8 +5,14 @@
  * The context keeps the reference's 96-byte layout (offsetof-checked in
  * tests/test_boundary.py) so code that embeds or memsets it is unaffected:
  *   totalLength @0 (bits), hash[5] @8, bufferLength @28, buffer @32.
- * The implementation lives in libsha1chunk.so (chunk_api.c); whole 64-byte
- * blocks are compressed by the gfx950 HIP engine, never on the host.
+ * The implementation lives in libsha1chunk.so (chunk_api.c).  Routing
+ * (include/sha1chunk.h, csrc/frontend.c): a SHA1Update/SHA1Final stream is
+ * one message, one serial chain of compressions, so by default its whole
+ * 64-byte blocks are compressed on the host (csrc/sha1_host.c: the x86 SHA
+ * extensions, ~2.5 GB/s a core, against ~85 MB/s for one GPU lane); a gfx950
+ * device is still required.  SHA1CHUNK_HOST_SMALL=0 sends them to the gfx950
+ * kernels (sha1chunk_compress_blocks); "<bytes>" hashes calls up to that
+ * size on the host and larger ones on the kernels.
  */
 #ifndef SHA1CHUNK_SHA_H
 #define SHA1CHUNK_SHA_H
@@ -33,7 +39,7 @@ extern "C" {
 
 /* sha.h:58 -- IV, zero counters. */
 void SHA1Init(SHA1Context *sc);
-/* sha.h:59 -- append len bytes; complete blocks go to the device engine. */
+/* sha.h:59 -- append len bytes; complete blocks are compressed as routed above. */
 void SHA1Update(SHA1Context *sc, const void *data, uint32_t len);
 /* sha.h:60 -- pad, append the 64-bit length, emit the big-endian digest
  * (hash may be NULL, as in the reference). */

@@ -200,11 +200,12 @@ int sha1chunk_synth_fill_ragged_async(void *d_base, const uint64_t *d_offsets,
  * created at a stream priority of their own (SHA1CHUNK_VQ_PRIO, default
  * "low"), so HIP maps them to other hardware queues than the caller's
  * default-priority streams: a persistent drain never sits in front of the
- * caller's own kernels.  Bound, tested (tests/test_gpu_vq_zero_copy.py::
- * test_wait_behind_busy_drains_is_bounded): a config-2 batch (4096 x
- * 512 KiB) launched on a fresh stream while four queues are continuously
- * fed finishes within its solo time + 10 ms; measured 6.25-6.47 ms against
- * 6.02 solo (12-26 ms with the queues' streams at the default priority).
+ * caller's own kernels.  Measured: a config-2 batch (4096 x 512 KiB)
+ * launched on a fresh stream while four queues are continuously fed took
+ * 6.25-6.47 ms against 6.02 solo (12-26 ms with the queues' streams at the
+ * default priority); tests/test_gpu_vq_zero_copy.py::
+ * test_wait_behind_busy_drains_is_bounded checks that the median stays
+ * within 1.5x of solo.
  *
  * Every queue call takes the queue's lock, so several threads (receive
  * sessions) may share one queue; a call that waits (for ring space, or
@@ -216,9 +217,12 @@ int sha1chunk_synth_fill_ragged_async(void *d_base, const uint64_t *d_offsets,
  * on SHA1CHUNK_VQ_THREADS threads (default 4, the caller included: three
  * helper threads per queue that spin briefly between submissions) when no
  * other submit is using them, else on the calling thread; reserve/commit
- * has no copy.  Measured on 16384 x 512 KiB host chunks from 4-8 receive
- * threads: 45-48 GiB/s reserve/commit, 22-25 GiB/s submit (DESIGN.md
- * section 9). */
+ * has no copy.  The helper threads run on the CPUs of the GPU's NUMA node
+ * (SHA1CHUNK_NUMA=off: anywhere); HIP's pinned allocation puts the ring's
+ * pages on that node already (measured, every page).
+ * Measured on 16384 x 512 KiB host chunks from 4 receive threads on the
+ * GPU's node: 39-47 GiB/s reserve/commit, 24-30 GiB/s submit, run to run
+ * (profiles/vq_place_r06*.jsonl). */
 typedef struct sha1chunk_vq sha1chunk_vq;
 /* NULL on failure (sha1chunk_last_error() says why). */
 sha1chunk_vq *sha1chunk_vq_create(size_t batch, uint32_t max_chunk_len);
@@ -233,11 +237,15 @@ int sha1chunk_vq_submit(sha1chunk_vq *q, const void *chunk, uint32_t len,
  * result is polled, until release() (after the caller copied the verified
  * chunk into its job buffer, reliable_udp.c:696-709, or dropped it).  A
  * reservation may also be released without a commit.  Unreleased buffers
- * hold ring space.  reserve() and submit() wait (bounded) for room while
- * in-flight chunks or other threads' reservations hold it; they fail (NULL,
- * resp. SHA1CHUNK_ENOMEM) rather than wait when the ring's oldest region is
- * the calling thread's own reservation, not committed or not released --
- * room only that thread could free.  In batch mode and
+ * hold ring space.  reserve() and submit() wait (bounded, SHA1CHUNK_VQ_WAIT_S,
+ * default 120 s) for room while in-flight chunks or other threads'
+ * reservations still filling hold it; they fail (NULL, resp.
+ * SHA1CHUNK_ENOMEM) rather than wait when the ring's oldest region is the
+ * calling thread's own reservation, not committed or not released -- room
+ * only that thread could free -- or, after a 2 ms grace, any thread's
+ * verified buffer whose result nobody has polled and released yet (room only
+ * a poll() and release() free: when every receive thread waits in reserve()
+ * nobody polls).  On NULL, poll, release and retry.  In batch mode and
  * on the batch-1 host path the buffer is ordinary host memory (commit
  * copies it, resp. hashes it in place). */
 void *sha1chunk_vq_reserve(sha1chunk_vq *q, uint32_t len);

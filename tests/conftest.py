@@ -65,3 +65,36 @@ def fixture_files():
         with tarfile.open(fileobj=io.BytesIO(files[name])) as t:
             files["example/" + gif] = t.extractfile(gif).read()
     return files
+
+
+# ---- bounds-checked backend runs ----------------------
+# SHA1CHUNK_CHECKED=1 with SHA1CHUNK_LIB=<dir>/libsha1chunk.so of `make
+# checked` (or `checked-unclamped`, the negative control): every GPU test
+# fails if the device counted an out-of-batch entry index or A.order value
+# during it (csrc/sha1_split.hpp checked_index; this process's calls only,
+# not those of child processes the test starts).
+def _checked_backend():
+    import ctypes
+    lib = os.environ.get("SHA1CHUNK_LIB")
+    path = os.environ.get("SHA1CHUNK_BACKEND") or (
+        os.path.join(os.path.dirname(os.path.abspath(lib)), "libsha1chunk_hip.so") if lib else None)
+    if not path:
+        raise RuntimeError("SHA1CHUNK_CHECKED=1 needs SHA1CHUNK_LIB (or SHA1CHUNK_BACKEND) of a checked build")
+    be = ctypes.CDLL(path)
+    if not hasattr(be, "s1be_checked_violations"):
+        raise RuntimeError(f"{path} is not a checked build (no s1be_checked_violations)")
+    be.s1be_checked_violations.restype = ctypes.c_longlong
+    be.s1be_checked_violations.argtypes = [ctypes.c_int]
+    return be
+
+
+@pytest.fixture(autouse=True)
+def _checked_bounds(request):
+    if os.environ.get("SHA1CHUNK_CHECKED") != "1" or request.node.get_closest_marker("gpu") is None:
+        yield
+        return
+    be = _checked_backend()
+    assert be.s1be_checked_violations(1) >= 0
+    yield
+    v = be.s1be_checked_violations(1)
+    assert v == 0, f"checked build: {v} out-of-batch entry index / A.order reads (device printf above)"
