@@ -12,8 +12,7 @@
 // (chunks of 4 MiB and more tie at the top in caller order; the planner then
 // prices such a group by its first chunk, the hashing is unaffected).
 //
-// Up to kSortMaxTiles tiles of 4096 chunks (1 Mi chunks) an LSD radix sort
-// of two 8-bit digits in four launches of its own:
+// An LSD radix sort of two 8-bit digits in four launches of its own:
 //   sort_hist<1>     keys, and each tile's low-digit histogram
 //   sort_scatter<1>  stable scatter by the low digit
 //   sort_hist<2>     each tile's high-digit histogram of that order (its
@@ -28,13 +27,14 @@
 // one with the same digit, from 8 ballots).  rocPRIM's radix sort took
 // ~51 us at 131072 chunks (a block sort and seven merge passes on 32-bit
 // lengths; onesweep on these 16-bit keys 58 us, profiles/sort_probe_r05.log).
-// Beyond 1 Mi chunks the columns grow with T, and rocPRIM's onesweep sorts
-// the same keys (same order: both stable).
+// Beyond kSortMaxTiles tiles (1 Mi chunks) the columns grow with T, so each
+// histogram launch is followed by hist_scan (one workgroup per slot: every
+// tile's start and the slot's total), and the scatters read those instead
+// of summing columns: six launches, the same order (round 6; rounds 5 sent
+// these batches to rocPRIM's onesweep).
 // Temporaries come from the stream-ordered allocator so concurrent calls on
 // different streams do not share scratch.
 #include <hip/hip_runtime.h>
-#include <rocprim/device/device_radix_sort.hpp>
-#include <rocprim/iterator/counting_iterator.hpp>
 #include <stdint.h>
 
 #include "sha1_kernels.h"
@@ -111,14 +111,47 @@ __global__ __launch_bounds__(kSortThreads) void sort_hist(const uint32_t* len, c
     if (tid < 256u) hist[blockIdx.x * 256u + tid] = h[tid];
 }
 
+// Batches of more than kSortMaxTiles tiles: slot blockIdx.x's count in the
+// tiles before each tile (pre[tile * 256 + slot]) and in all of them
+// (tot[slot]), an exclusive scan down the histogram column.
+constexpr uint32_t kScanThreads = 256;
+__global__ __launch_bounds__(kScanThreads) void hist_scan(const uint32_t* hist, uint32_t tiles, uint32_t* pre,
+                                                          uint32_t* tot) {
+    __shared__ uint32_t wsum[kScanThreads / 64];
+    const uint32_t s = blockIdx.x, tid = threadIdx.x, lane = tid & 63u, wave = tid >> 6;
+    const uint32_t per = (tiles + kScanThreads - 1u) / kScanThreads;
+    const uint32_t t0 = min(tiles, tid * per), t1 = min(tiles, t0 + per);
+    uint32_t sum = 0;
+    for (uint32_t t = t0; t < t1; ++t) sum += hist[t * 256u + s];
+    uint32_t inc = sum;
+#pragma unroll
+    for (uint32_t d = 1; d < 64u; d <<= 1) {
+        const uint32_t v = __shfl_up(inc, d);
+        if (lane >= d) inc += v;
+    }
+    if (lane == 63u) wsum[wave] = inc;
+    __syncthreads();
+    uint32_t run = inc - sum;
+    for (uint32_t w = 0; w < wave; ++w) run += wsum[w];
+    for (uint32_t t = t0; t < t1; ++t) {
+        const uint32_t v = hist[t * 256u + s];
+        pre[t * 256u + s] = run;
+        run += v;
+    }
+    if (tid == kScanThreads - 1u) tot[s] = run;
+}
+
 // One stable counting-sort pass over digit PASS of tile blockIdx.x (keys_in
 // / ids_in in the previous pass's order; ids_in null = the chunk index):
 // PASS 1 writes keys_out / ids_out, PASS 2 the order and sorted lengths.
+// pre_in / tot_in (batches of more than kSortMaxTiles tiles): the tile's
+// per-slot starts and the slot totals from hist_scan; null: summed here.
 template <int PASS>
 __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint16_t* keys_in, const uint32_t* ids_in,
                                                              const uint32_t* hist, uint32_t tiles, uint32_t n,
                                                              uint16_t* keys_out, uint32_t* ids_out,
-                                                             const uint32_t* len, uint32_t* sorted_len) {
+                                                             const uint32_t* len, uint32_t* sorted_len,
+                                                             const uint32_t* pre_in, const uint32_t* tot_in) {
     __shared__ uint32_t start[256];                   // the tile's first position per slot
     __shared__ uint32_t part_tot[4][256], part_pre[4][256], wsum[4];
     __shared__ uint16_t cnt[kSortSlices][256];        // per (item, wave) slice, then its prefix
@@ -129,8 +162,12 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint16_t* key
     // count in all of them and in those before this one
     {
         const uint32_t s = tid & 255u, q = tid >> 8, per = (tiles + 3u) / 4u;
-        const uint32_t t0 = min(tiles, q * per), t1 = min(tiles, t0 + per);
+        const uint32_t t0 = pre_in ? tiles : min(tiles, q * per), t1 = pre_in ? tiles : min(tiles, t0 + per);
         uint32_t tot = 0, pre = 0, t = t0;
+        if (pre_in && q == 0u) {
+            tot = tot_in[s];
+            pre = pre_in[tile * 256u + s];
+        }
         for (; t + 8u <= t1; t += 8u) {
             uint32_t v[8];
 #pragma unroll
@@ -230,12 +267,6 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint16_t* key
     }
 }
 
-// Batches beyond kSortMaxTiles tiles: rocPRIM onesweep on the same keys.
-__global__ void block_keys16(const uint32_t* len, uint16_t* key, uint32_t n) {
-    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i < n) key[i] = block_key(len[i]);
-}
-
 // sorted_len[i] = len[order[i]]: the planner's view of the sorted batch.
 __global__ void gather_lengths(const uint32_t* len, const uint32_t* order, uint32_t* out, uint32_t n) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -250,24 +281,17 @@ hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t
     *d_plan = nullptr;
     *scratch = nullptr;
     const uint32_t tiles = (uint32_t)((uint64_t(n) + kSortTile - 1u) / kSortTile);
-    const bool own = tiles <= kSortMaxTiles;
-    const rocprim::counting_iterator<uint32_t> ids(0u);
+    const bool scan = tiles > kSortMaxTiles;  // starts from hist_scan, not summed per workgroup
     const size_t hb = align256(size_t(tiles) * 256u * sizeof(uint32_t));
-    size_t temp_bytes = 0;
-    hipError_t e = hipSuccess;
-    if (own) {
-        temp_bytes = 2 * hb + align256(size_t(n) * sizeof(uint32_t));
-    } else {
-        e = rocprim::radix_sort_pairs_desc(nullptr, temp_bytes, (const uint16_t*)nullptr, (uint16_t*)nullptr, ids,
-                                           (uint32_t*)nullptr, n, 0, 16, st);
-        if (e != hipSuccess) return e;
-    }
+    const size_t tb = align256(256u * sizeof(uint32_t));
+    // temporaries: hist1, hist2, ids2 [, pre1, pre2, tot1, tot2]
+    const size_t temp_bytes = 2 * hb + align256(size_t(n) * sizeof(uint32_t)) + (scan ? 2 * hb + 2 * tb : 0);
     // [sorted lengths][order][plan][keys][keys'][temporaries]
     const size_t arr = align256(size_t(n) * sizeof(uint32_t));
     const size_t arr16 = align256(size_t(n) * sizeof(uint16_t));
     const size_t planb = mixed_plan_bytes(n);
     void* mem = nullptr;
-    e = hipMallocAsync(&mem, 2 * arr + planb + 2 * arr16 + align256(temp_bytes), st);
+    hipError_t e = hipMallocAsync(&mem, 2 * arr + planb + 2 * arr16 + temp_bytes, st);
     if (e != hipSuccess) return e;
     uint8_t* b = static_cast<uint8_t*>(mem);
     uint32_t* sorted_len = reinterpret_cast<uint32_t*>(b);
@@ -276,28 +300,25 @@ hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t
     uint16_t* keys = reinterpret_cast<uint16_t*>(b + 2 * arr + planb);
     uint16_t* keys2 = reinterpret_cast<uint16_t*>(b + 2 * arr + planb + arr16);
     uint8_t* temp = b + 2 * arr + planb + 2 * arr16;
-    if (own) {
-        uint32_t* hist1 = reinterpret_cast<uint32_t*>(temp);
-        uint32_t* hist2 = reinterpret_cast<uint32_t*>(temp + hb);
-        uint32_t* ids2 = reinterpret_cast<uint32_t*>(temp + 2 * hb);
-        hipLaunchKernelGGL(sort_hist<1>, dim3(tiles), dim3(kSortThreads), 0, st, d_len, (const uint16_t*)nullptr,
-                           keys, hist1, n);
-        hipLaunchKernelGGL(sort_scatter<1>, dim3(tiles), dim3(kSortThreads), 0, st, keys, (const uint32_t*)nullptr,
-                           hist1, tiles, n, keys2, ids2, (const uint32_t*)nullptr, (uint32_t*)nullptr);
-        hipLaunchKernelGGL(sort_hist<2>, dim3(tiles), dim3(kSortThreads), 0, st, (const uint32_t*)nullptr, keys2,
-                           (uint16_t*)nullptr, hist2, n);
-        hipLaunchKernelGGL(sort_scatter<2>, dim3(tiles), dim3(kSortThreads), 0, st, keys2, ids2, hist2, tiles, n,
-                           (uint16_t*)nullptr, order, d_len, sorted_len);
-        e = hipGetLastError();
-    } else {
-        const dim3 grid((n + 255u) / 256u);
-        hipLaunchKernelGGL(block_keys16, grid, dim3(256), 0, st, d_len, keys, n);
-        e = rocprim::radix_sort_pairs_desc(temp, temp_bytes, keys, keys2, ids, order, n, 0, 16, st);
-        if (e == hipSuccess) {
-            hipLaunchKernelGGL(gather_lengths, grid, dim3(256), 0, st, d_len, order, sorted_len, n);
-            e = hipGetLastError();
-        }
-    }
+    uint32_t* hist1 = reinterpret_cast<uint32_t*>(temp);
+    uint32_t* hist2 = reinterpret_cast<uint32_t*>(temp + hb);
+    uint32_t* ids2 = reinterpret_cast<uint32_t*>(temp + 2 * hb);
+    uint8_t* extra = temp + 2 * hb + align256(size_t(n) * sizeof(uint32_t));
+    uint32_t* pre1 = scan ? reinterpret_cast<uint32_t*>(extra) : nullptr;
+    uint32_t* pre2 = scan ? reinterpret_cast<uint32_t*>(extra + hb) : nullptr;
+    uint32_t* tot1 = scan ? reinterpret_cast<uint32_t*>(extra + 2 * hb) : nullptr;
+    uint32_t* tot2 = scan ? reinterpret_cast<uint32_t*>(extra + 2 * hb + tb) : nullptr;
+    hipLaunchKernelGGL(sort_hist<1>, dim3(tiles), dim3(kSortThreads), 0, st, d_len, (const uint16_t*)nullptr, keys,
+                       hist1, n);
+    if (scan) hipLaunchKernelGGL(hist_scan, dim3(256), dim3(kScanThreads), 0, st, hist1, tiles, pre1, tot1);
+    hipLaunchKernelGGL(sort_scatter<1>, dim3(tiles), dim3(kSortThreads), 0, st, keys, (const uint32_t*)nullptr, hist1,
+                       tiles, n, keys2, ids2, (const uint32_t*)nullptr, (uint32_t*)nullptr, pre1, tot1);
+    hipLaunchKernelGGL(sort_hist<2>, dim3(tiles), dim3(kSortThreads), 0, st, (const uint32_t*)nullptr, keys2,
+                       (uint16_t*)nullptr, hist2, n);
+    if (scan) hipLaunchKernelGGL(hist_scan, dim3(256), dim3(kScanThreads), 0, st, hist2, tiles, pre2, tot2);
+    hipLaunchKernelGGL(sort_scatter<2>, dim3(tiles), dim3(kSortThreads), 0, st, keys2, ids2, hist2, tiles, n,
+                       (uint16_t*)nullptr, order, d_len, sorted_len, pre2, tot2);
+    e = hipGetLastError();
     if (e != hipSuccess) {
         (void)hipFreeAsync(mem, st);
         return e;

@@ -844,6 +844,38 @@ def test_verify_chunk_hash_ragged_master_and_mismatch(pkg, dev, oracle, verify_d
     assert d.returncode == 0, d.stderr
 
 
+def test_verify_chunk_hash_index_default_routing(pkg, dev, oracle, verify_driver, tmp_path):
+    """Round 6: the master index is built through sha1chunk_hash_fd (the
+    parallel pread pipeline) and a short last chunk re-hashed zero-padded.
+    A 9-chunk master with a ragged tail (above the 4 MiB host cut, so the
+    default routing builds the table on the kernels and pads the tail on the
+    host), every chunk requested in a scattered order: the same stdout and
+    stream positions as the per-call path, every digest the zero-padded
+    hashlib one, and a wrong digest served from the table still exits(-1)."""
+    import hashlib
+    size = 9 * L512 + 77777
+    data = oracle.synth_chunks(1200, 10, L512).tobytes()[:size]
+    p = tmp_path / "master9.dat"
+    p.write_bytes(data)
+    padded = data + bytes(10 * L512 - size)
+    hexes = [hashlib.sha1(padded[i * L512:(i + 1) * L512]).hexdigest() for i in range(10)]
+    order = [9, 0, 9, 4, 8, 1, 7, 2, 6, 3, 5, 9]
+    pairs = [(i, hexes[i]) for i in order]
+
+    def run(index, extra=()):
+        env = default_env(SHA1CHUNK_MASTER_INDEX="1" if index else "0", SHA1CHUNK_MASTER_SETTLE_MS="0")
+        args = [verify_driver, str(p)] + [x for i, h in list(pairs) + list(extra) for x in (str(i), h)]
+        return subprocess.run(args, capture_output=True, text=True, env=env, timeout=120)
+
+    a, b = run(True), run(False)
+    assert a.returncode == 0 and b.returncode == 0, (a.stderr, b.stderr)
+    assert a.stdout == b.stdout and a.stdout.count("ok ") == len(pairs)
+    bad = hexes[4][:-1] + ("0" if hexes[4][-1] != "0" else "1")
+    c = run(True, [(4, bad)])
+    assert c.returncode == 255 and "Unmatched chunk hashes" in c.stderr
+    assert c.stdout.count("ok ") == len(pairs)
+
+
 @pytest.mark.parametrize("settle_ms", ["0", "2000"])
 def test_verify_chunk_hash_index_not_stale(pkg, dev, oracle, verify_driver, tmp_path, settle_ms):
     """The sender re-verifies every GET against the master file (chunk.c:

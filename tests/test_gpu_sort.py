@@ -3,9 +3,10 @@ descending SHA-1 block counts, ceil((len + 9) / 64) clamped at 65535, ties
 in caller order -- numpy's stable argsort of the same keys, position for
 position, and the sorted lengths the planner reads.  Tile edges of the
 three-kernel radix sort (4096 chunks), all-equal and all-distinct keys,
-empty chunks, chunks of 4 MiB and more (clamped keys tie), and the rocPRIM
-path beyond 1 Mi chunks.  Through the backend's diagnostics entry point
-s1be_sort_order_async (no frontend symbol)."""
+empty chunks, chunks of 4 MiB and more (clamped keys tie), and the scanned
+path beyond 1 Mi chunks (hist_scan starts instead of per-workgroup column
+sums; rocPRIM's onesweep before round 6).  Through the backend's diagnostics
+entry point s1be_sort_order_async (no frontend symbol)."""
 import ctypes as C
 import os
 
@@ -82,12 +83,18 @@ def test_ties_and_clamp(sort_order):
     check(sort_order, (np.arange(70000, dtype=np.uint32)[::-1] * 64).copy())  # already sorted
 
 
-def test_rocprim_path_beyond_1mi(sort_order):
-    """Past 256 tiles of 4096 the same keys go through rocPRIM's onesweep:
-    the same order."""
-    rng = np.random.default_rng(11)
-    n = (1 << 20) + 4097
-    lens = rng.integers(0, 300000, n).astype(np.uint32)
+@pytest.mark.parametrize("n", [(1 << 20) + 1, (1 << 20) + 4097, 3 * (1 << 20) + 12345])
+def test_scan_path_beyond_1mi(sort_order, n):
+    """Past 256 tiles of 4096 the tile starts come from hist_scan (one
+    workgroup per slot) instead of each scatter workgroup's column sums: the
+    same stable order, at one chunk past the cut, a partial tile past it, and
+    ~3 Mi chunks of the config-5 law with clamped 8 MiB chunks and empties."""
+    rng = np.random.default_rng(n)
+    if n < (1 << 21):
+        lens = rng.integers(0, 300000, n).astype(np.uint32)
+    else:
+        lens = np.exp(rng.uniform(np.log(4096), np.log(1 << 20), n)).astype(np.uint32)
+        lens[rng.choice(n, 500, replace=False)] = 0
     lens[rng.choice(n, 1000, replace=False)] = 1 << 23
     check(sort_order, lens)
 
