@@ -2066,7 +2066,7 @@ int pvq_alloc(Pvq* P, uint32_t len, bool reserved, uint64_t* id) {
     // it as for any in-flight group (bounded, pvq_wait).
     const std::thread::id me = std::this_thread::get_id();
     std::chrono::steady_clock::time_point held_since{};
-    bool held_seen = false;
+    uint64_t held_id = ~0ull;  // the head region the grace is running for
     auto stuck = [&]() -> const char* {
         if (P->regions.empty()) return nullptr;
         const PvqRegion& r = P->regions.front();
@@ -2076,8 +2076,8 @@ int pvq_alloc(Pvq* P, uint32_t len, bool reserved, uint64_t* id) {
         if (!r.collected) return nullptr;
         if (r.owner == me) return own;
         const auto now = std::chrono::steady_clock::now();
-        if (!held_seen) {
-            held_seen = true;
+        if (held_id != P->reg_base) {  // a new head region: its own grace
+            held_id = P->reg_base;
             held_since = now;
         }
         return now - held_since >= kHeldResultWait

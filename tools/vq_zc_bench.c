@@ -191,7 +191,7 @@ static struct {
     int local_src;     /* producers write their own source chunks */
     cpu_set_t pin_set;
     int cpu0[64], cpu1[64];
-    void *own_page[64];
+    int own_node[64]; /* submit: the node of each producer's session buffer (-1 unknown) */
 } B;
 
 static void fail_msg(const char *what) {
@@ -232,10 +232,7 @@ static void *producer(void *arg) {
         for (size_t c = (size_t)t; c < B.distinct; c += (size_t)B.threads)
             synth_chunk(B.src + c * (size_t)L512, c);
     uint8_t *own = B.mode == 1 ? (uint8_t *)malloc(L512) : NULL;
-    if (own) {
-        memset(own, 0, L512);
-        if (t < 64) B.own_page[t] = own;
-    }
+    if (own) memset(own, 0, L512); /* first touch by this producer */
     pthread_barrier_wait(&B.start);
     if (t < 64) B.cpu0[t] = sched_getcpu();
     size_t since = 0;
@@ -273,10 +270,9 @@ static void *producer(void *arg) {
     if (own && t < 64) {
         long h[MAXNODE + 1] = {0};
         range_hist(own, L512, 4096, h);
-        int k = MAXNODE;
+        B.own_node[t] = -1;
         for (int j = 0; j < MAXNODE; ++j)
-            if (h[j]) k = j;
-        B.own_page[t] = (void *)(intptr_t)k;  /* reused: the buffer's node */
+            if (h[j]) B.own_node[t] = j;
     }
     free(own);
     return NULL;
@@ -410,10 +406,7 @@ int main(int argc, char **argv) {
     printf("], ");
     if (B.mode == 1) {
         printf("\"submit_buffer_nodes\": [");
-        for (int t = 0; t < B.threads && t < 64; ++t) {
-            const int k = (int)(intptr_t)B.own_page[t];
-            printf("%s%d", t ? ", " : "", k < MAXNODE ? k : -1);
-        }
+        for (int t = 0; t < B.threads && t < 64; ++t) printf("%s%d", t ? ", " : "", B.own_node[t]);
         printf("], ");
     }
     put_hist(stdout, "ring_pages", ring_h);
