@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cctype>
 #include <chrono>
 #include <condition_variable>
 #include <cerrno>
@@ -30,6 +31,7 @@
 #include <thread>
 #include <tuple>
 #include <unordered_map>
+#include <sched.h>
 #include <sys/stat.h>
 #include <unistd.h>
 #include <vector>
