@@ -355,7 +355,7 @@ def main():
         result["config4_shard8"] = _shard_leg(pkg, shard, torch, golden, 8, 1, a)
         result["config4_shard2"] = _shard_leg(pkg, shard, torch, golden, 2, 1, a)
         result["strong_projection"] = _strong_projection(result)
-    fpath = None
+    fpath, reqs = None, None
     try:
         if rank == 0 and world == 1 and not a.no_configs:
             # the other BASELINE configs on this GPU, each checked against the
@@ -365,9 +365,17 @@ def main():
             result["config1"] = _config1_leg(golden)
             result["verify_queue"] = _verify_queue_leg(result["config3_e2e"].get("pinned_h2d_GiBps"))
             if a.file_chunks > 0:
-                fpath = _write_corpus_file(pkg, torch, a.file_chunks)
-                result["file"], fdig = _file_leg(pkg, fpath, golden, result["config3_e2e"].get("pinned_h2d_GiBps"))
-                result["master_verify"], reqs = _master_verify_leg(fpath, fdig)
+                # a failed file leg must not cost the bench line (no room for
+                # the temp file, a tool missing): its object says why
+                try:
+                    fpath = _write_corpus_file(pkg, torch, a.file_chunks)
+                    result["file"], fdig = _file_leg(pkg, fpath, golden,
+                                                     result["config3_e2e"].get("pinned_h2d_GiBps"))
+                    result["master_verify"], reqs = _master_verify_leg(fpath, fdig)
+                except Exception as e:
+                    result.setdefault("file", {"error": repr(e)[:300]})
+                    if fpath and "master_verify" not in result:
+                        result["master_verify"] = {"error": repr(e)[:300]}
         if rank == 0 and world == 1 and not a.no_latency:
             result["latency_one_chunk"] = _latency_one_chunk(dev)
         if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -383,7 +391,7 @@ def main():
                 c1["reference_cli_median_ms"] = ref["median_ms"]
                 for k in ("default", "device", "host_small"):
                     c1[k]["vs_reference"] = round(c1[k]["median_ms"] / ref["median_ms"], 3)
-            if fpath and "master_verify" in result:
+            if fpath and reqs:
                 ref = _reference_master_verify(fpath, reqs)
                 result["cpu_baseline"]["master_verify_reference"] = ref
                 mv = result["master_verify"]
@@ -393,7 +401,7 @@ def main():
                 if ref.get("O0", {}).get("rest_median_ms") and mv.get("index", {}).get("rest_median_ms"):
                     mv["index_speedup_vs_reference_O0"] = round(
                         ref["O0"]["rest_median_ms"] / mv["index"]["rest_median_ms"], 1)
-            if fpath and "file" in result:
+            if fpath and "cli" in result.get("file", {}):
                 ref = _reference_file_cli(fpath)
                 result["cpu_baseline"]["file_reference_cli"] = ref
                 if ref.get("GiBps"):
@@ -401,7 +409,7 @@ def main():
                     fl["reference_cli_GiBps"] = ref["GiBps"]
                     fl["cli_vs_reference"] = round(fl["cli"]["GiBps"] / ref["GiBps"], 1)
     finally:
-        if fpath:
+        if fpath and os.path.exists(fpath):
             os.unlink(fpath)
     if use_pg:
         result["config"]["control_plane"] = f"torch.distributed {backend}, world {world}"
@@ -914,7 +922,12 @@ def _verify_queue_leg(h2d_gibps, runs: int = 3) -> dict:
 def _write_corpus_file(pkg, torch, chunks: int) -> str:
     """Chunks 0..chunks-1 of the synthetic corpus (config 3's first chunks),
     generated on the device, written to a temp file ($TMPDIR)."""
+    import shutil
     import tempfile
+    need = chunks * CHUNK_LEN
+    free = shutil.disk_usage(tempfile.gettempdir()).free
+    if free < need + (1 << 30):
+        raise RuntimeError(f"{tempfile.gettempdir()}: {free} bytes free, the file leg needs {need} + 1 GiB")
     fd, path = tempfile.mkstemp(prefix="sha1bench_file_", suffix=".dat")
     piece = 1024
     tmp = torch.empty(piece * CHUNK_LEN, dtype=torch.uint8, device="cuda")
