@@ -9,6 +9,7 @@
 #include <atomic>
 #include <condition_variable>
 #include <cstdint>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <mutex>
@@ -134,6 +135,35 @@ private:
     std::atomic<uint64_t> next_{0};  // job << 32 | next part index
     std::atomic<size_t> left_{0};
 };
+
+// The CPUs of a sysfs cpulist ("0-63,128-191\n") that are also in `allowed`,
+// into *out; returns their count (malformed pieces are skipped).  The
+// runtime's NUMA placement (sha1_runtime.hip near_cpus) reads the GPU's
+// node's list with it.
+inline int cpus_from_list(const char* list, const cpu_set_t& allowed, cpu_set_t* out) {
+    CPU_ZERO(out);
+    for (const char* p = list; p && *p;) {
+        char* end = nullptr;
+        const long a = strtol(p, &end, 10);
+        if (end == p) {  // not a number: skip to the next piece
+            p = strchr(p, ',');
+            if (p) ++p;
+            continue;
+        }
+        long b = a;
+        p = end;
+        if (*p == '-') {
+            b = strtol(p + 1, &end, 10);
+            if (end == p + 1) b = a;  // "5-": just 5
+            p = end;
+        }
+        for (long c = a; c <= b && c >= 0 && c < CPU_SETSIZE; ++c)
+            if (CPU_ISSET(static_cast<int>(c), &allowed)) CPU_SET(static_cast<int>(c), out);
+        p = strchr(p, ',');
+        if (p) ++p;
+    }
+    return CPU_COUNT(out);
+}
 
 // memcpy split over a pool (pieces of >= 64 KiB)
 inline void pool_copy(PartPool& pool, uint8_t* dst, const uint8_t* src, size_t n) {

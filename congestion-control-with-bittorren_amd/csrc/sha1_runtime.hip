@@ -51,7 +51,7 @@ using s1host::PartPool;
 // places it on the GPU's node: profiles/vq_place_r06*.jsonl) and the GPU that
 // reads it.  SHA1CHUNK_NUMA=off (or 0) leaves them to the scheduler.
 // nullptr: no placement (off, one node, node unknown, or none of its CPUs
-// allowed).
+// allowed, or fewer than four).
 const cpu_set_t* near_cpus(int id) {
     struct Near {
         std::once_flag once;
@@ -86,17 +86,10 @@ const cpu_set_t* near_cpus(int id) {
         }
         cpu_set_t allowed, mine;
         if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return;
-        CPU_ZERO(&mine);
-        for (char* save = nullptr, *tok = strtok_r(list, ",\n", &save); tok; tok = strtok_r(nullptr, ",\n", &save)) {
-            int a = 0, b = 0;
-            const int k = sscanf(tok, "%d-%d", &a, &b);
-            if (k < 1) continue;
-            if (k == 1) b = a;
-            for (int c = a; c <= b && c < CPU_SETSIZE; ++c)
-                if (CPU_ISSET(c, &allowed)) CPU_SET(c, &mine);
-        }
-        // nothing to gain when every allowed CPU is on this node already
-        if (CPU_COUNT(&mine) == 0 || CPU_EQUAL(&mine, &allowed)) return;
+        // nothing to gain when every allowed CPU is on this node already,
+        // and no piling of a pool's helpers onto fewer than kMinNearCpus
+        constexpr int kMinNearCpus = 4;
+        if (s1host::cpus_from_list(list, allowed, &mine) < kMinNearCpus || CPU_EQUAL(&mine, &allowed)) return;
         n.set = mine;
         n.ok = true;
     });

@@ -10,7 +10,8 @@ code with sanitizers instead).  CPU only:
   line without a hash and a hash that is absent;
 * the runtime's host thread pool (csrc/part_pool.hpp: verify-queue copies,
   pageable packing, parallel file reads) under ThreadSanitizer, hammered
-  with back-to-back jobs of every width while helpers spin or sleep.
+  with back-to-back jobs of every width while helpers spin or sleep; its
+  cpulist parser and helpers pinned to a CPU set (the NUMA placement).
 Any sanitizer report fails the run (halt_on_error, exit code != 0)."""
 import hashlib
 import os
@@ -145,6 +146,8 @@ _POOL_DRV = r'''
 #include <cstdio>
 #include <cstdlib>
 #include <vector>
+#include <pthread.h>
+#include <sched.h>
 #include "part_pool.hpp"
 using s1host::PartPool;
 int main() {
@@ -168,6 +171,41 @@ int main() {
                 nanosleep(&ts, nullptr);
             }
         }
+    }
+    // cpulist parsing (the runtime's NUMA placement reads the GPU node's list)
+    {
+        cpu_set_t all, some, out;
+        CPU_ZERO(&all);
+        for (int c = 0; c < 64; ++c) CPU_SET(c, &all);
+        CPU_ZERO(&some);
+        for (int c : {2, 3, 8, 40}) CPU_SET(c, &some);
+        bad += s1host::cpus_from_list("0-3,8,10-11\n", all, &out) != 7;
+        for (int c : {0, 1, 2, 3, 8, 10, 11}) bad += !CPU_ISSET(c, &out);
+        bad += s1host::cpus_from_list("0-63,128-191\n", some, &out) != 4;
+        bad += s1host::cpus_from_list("x,5,,7-,9-8,12-13", all, &out) != 4;  // 5, 7, 12, 13
+        for (int c : {5, 7, 12, 13}) bad += !CPU_ISSET(c, &out);
+        bad += s1host::cpus_from_list("", all, &out) != 0;
+    }
+    // helpers pinned to a CPU set run their parts there (the caller's own
+    // parts run wherever the caller runs)
+    {
+        cpu_set_t aff, pin;
+        sched_getaffinity(0, sizeof aff, &aff);
+        CPU_ZERO(&pin);
+        int first = -1;
+        for (int c = 0; c < CPU_SETSIZE && first < 0; ++c)
+            if (CPU_ISSET(c, &aff)) first = c;
+        CPU_SET(first, &pin);
+        PartPool pool(3, &pin);
+        const pthread_t me = pthread_self();
+        std::vector<int> where(4096, -2);
+        std::vector<char> by_helper(4096, 0);
+        for (int job = 0; job < 20; ++job)
+            pool.run(where.size(), [&](size_t i) {
+                where[i] = sched_getcpu();
+                by_helper[i] = !pthread_equal(pthread_self(), me);
+            });
+        for (size_t i = 0; i < where.size(); ++i) bad += by_helper[i] && where[i] != first;
     }
     std::printf("pool %s\n", bad ? "BAD" : "ok");
     return bad ? 1 : 0;
