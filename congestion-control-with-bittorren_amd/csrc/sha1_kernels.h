@@ -44,8 +44,28 @@ hipError_t launch_split_study(const BatchArgs& A, int unit_blocks, hipStream_t s
 // them all in the 8-wave split shape (sha1_kernels.hip, mixed).  `plan`:
 // 3 device words; forced (or null): {mode, H, F} instead of the planner's.
 uint32_t mixed_grid(uint32_t groups, int cus, uint32_t* hcap);
-hipError_t launch_mixed(const BatchArgs& A, const uint32_t* sorted_len, uint32_t* plan, int cus,
+// Exact order of the chunks whose 16-bit sort keys clamp (>= 65535 SHA-1
+// blocks: 4 MiB and more).  The sort leaves them at the front in caller
+// order; the mixed path's layout kernel re-ranks up to kBigExact of them by
+// their exact block counts (stable) before the planner and the hash kernel
+// read the order (sha1_kernels.hip plan_layout_kernel).  More than that
+// keep caller order among themselves (digests unaffected).
+constexpr uint32_t kBigExact = 4096;
+struct BigFix {
+    const uint32_t* cnt;   // per sort tile: its chunks whose key clamped (sort_hist<1>)
+    uint32_t tiles;
+    const uint32_t* len;   // positions [0, min(m, kBigExact)) of the sort's output:
+    const uint32_t* id;    //   their lengths and chunk ids (sort_scatter<2>)
+    uint32_t* order;       // the sort's order and (group-head) sorted lengths,
+    uint32_t* sorted_len;  //   rewritten for positions < m
+};
+// big (or null: no re-ranking): the sort's BigFix.
+hipError_t launch_mixed(const BatchArgs& A, const uint32_t* sorted_len, const BigFix* big, uint32_t* plan, int cus,
                         const int* forced, hipStream_t st);
+// The layout summary alone (its re-ranking included): the diagnostics of
+// s1be_mixed_order_async.
+hipError_t launch_plan_layout(const BatchArgs& A, const uint32_t* sorted_len, const BigFix* big, uint32_t* plan,
+                              hipStream_t st);
 // Persistent verify-queue drain (sha1_kernels.hip, vq drain; host side in
 // sha1_runtime.hip, the persistent sha1chunk_vq).  The queue's rings live in
 // coherent pinned host memory, which the kernel reads over PCIe (no copy
@@ -88,8 +108,9 @@ inline size_t mixed_plan_bytes(uint32_t n) {
     const size_t words = ((size_t(n) + 63) / 64 + 31) / 32;  // one per 32 groups of 64 chunks
     return 256 + ((words * 12 + 255) & ~size_t(255));
 }
+// big (or null): receives the clamped chunks' re-ranking inputs (BigFix).
 hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t** d_order,
-                               const uint32_t** d_sorted_len, uint32_t** d_plan, void** scratch,
+                               const uint32_t** d_sorted_len, uint32_t** d_plan, void** scratch, BigFix* big,
                                hipStream_t st);
 // out[i] = len[order[i]] for every i (diagnostics: s1be_sort_order_async).
 hipError_t gather_sorted_lengths(const uint32_t* d_len, const uint32_t* d_order, uint32_t* d_out, uint32_t n,

@@ -378,11 +378,23 @@ __device__ __forceinline__ uint32_t plan_blocks(const uint32_t* sorted_len, cons
 constexpr int kLayoutThreads = 1024;  // two groups per wave (eight at 256 threads: 16.5 us at 2048 groups)
 constexpr uint32_t kLayoutGroupsPerWave = 32 / (kLayoutThreads / 64);
 
+// The workgroups holding positions below kBigExact (2048 per workgroup)
+// first re-rank the chunks whose sort keys clamped (BigFix, sha1_kernels.h):
+// m = the tiles' clamped counts summed; for 0 < m <= kBigExact every such
+// workgroup sorts the m (exact block count, caller position) pairs in LDS
+// (bitonic) and rewrites the order, and the group-head sorted lengths, of its
+// own positions below m, then summarises its groups from the re-ranked
+// entries.  No other workgroup, and no batch without chunks of 4 MiB and
+// more, does anything extra.
+constexpr uint32_t kLayoutPositions = 32u * 64u;  // positions per layout workgroup
+
 __global__ __launch_bounds__(kLayoutThreads) void plan_layout_kernel(BatchArgs A, const uint32_t* sorted_len,
-                                                                     uint64_t* tb, uint32_t* bits) {
+                                                                     BigFix B, uint64_t* tb, uint32_t* bits) {
     const uint32_t lane = threadIdx.x % 64u, wave = threadIdx.x / 64u;
     const uint32_t G = (A.n + 63u) / 64u;
     __shared__ uint32_t tog[32], blk[32];
+    __shared__ uint64_t bk[kBigExact];  // (0x7ffffff - blocks) << 32 | caller position, sorted
+    __shared__ uint32_t bm;
     // The wave's groups' entries first, all in flight together: each is two
     // dependent global reads (order, then offset and length), and taking
     // the groups one at a time cost ~17 us at 2048 groups.
@@ -395,6 +407,60 @@ __global__ __launch_bounds__(kLayoutThreads) void plan_layout_kernel(BatchArgs A
         } else {
             en[k].p = nullptr;
             en[k].len = 0;
+        }
+    }
+    uint32_t mfix = 0;  // positions below this were re-ranked here (their heads' blocks in bk)
+    // position 0 holds the largest key: below the clamp, no chunk clamped and
+    // nothing more to read (one load, in flight with the entries')
+    if (B.cnt && blockIdx.x * kLayoutPositions < kBigExact && total_blocks(sorted_len[0]) >= 65535u) {
+        const uint32_t t = threadIdx.x;
+        if (t < 64u) {
+            uint32_t v = 0;
+            for (uint32_t i = t; i < B.tiles; i += 64u) v += B.cnt[i];
+#pragma unroll
+            for (uint32_t o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+            if (t == 0) bm = v;
+        }
+        __syncthreads();
+        const uint32_t m = bm;
+        if (m > 0 && m <= kBigExact && blockIdx.x * kLayoutPositions < m) {
+            uint32_t P = 64;
+            while (P < m) P <<= 1;
+            for (uint32_t j = t; j < P; j += kLayoutThreads)
+                bk[j] = j < m ? (uint64_t)(0x07ffffffu - total_blocks(B.len[j])) << 32 | j : ~0ull;
+            __syncthreads();
+            // ascending bitonic sort: longest first, then caller order
+            for (uint32_t k2 = 2; k2 <= P; k2 <<= 1)
+                for (uint32_t j2 = k2 >> 1; j2 > 0; j2 >>= 1) {
+                    for (uint32_t i = t; i < P; i += kLayoutThreads) {
+                        const uint32_t ixj = i ^ j2;
+                        if (ixj > i) {
+                            const uint64_t a = bk[i], b = bk[ixj];
+                            if ((a > b) == ((i & k2) == 0u)) {
+                                bk[i] = b;
+                                bk[ixj] = a;
+                            }
+                        }
+                    }
+                    __syncthreads();
+                }
+            const uint32_t r0 = blockIdx.x * kLayoutPositions, r1 = min(m, r0 + kLayoutPositions);
+            for (uint32_t r = r0 + t; r < r1; r += kLayoutThreads) {
+                const uint32_t j = static_cast<uint32_t>(bk[r]);
+                B.order[r] = B.id[j];
+                if ((r & 63u) == 0u) B.sorted_len[r] = B.len[j];
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < kLayoutGroupsPerWave; ++k) {
+                const uint32_t e = 64u * (32u * blockIdx.x + wave * kLayoutGroupsPerWave + k) + lane;
+                if (e < m) {
+                    const uint32_t j = static_cast<uint32_t>(bk[e]);
+                    const uint32_t id = B.id[j];
+                    en[k].p = A.base + A.off[id];
+                    en[k].len = B.len[j];
+                }
+            }
+            mfix = m;
         }
     }
 #pragma unroll
@@ -420,7 +486,10 @@ __global__ __launch_bounds__(kLayoutThreads) void plan_layout_kernel(BatchArgs A
         }
         if (lane == 0) {
             tog[slot] = hi - lo <= 2 * bytes + (2ull << 20) ? 1u : 0u;
-            blk[slot] = group_blocks(sorted_len, g);
+            // a re-ranked head's blocks from LDS (its sorted_len was rewritten
+            // just now by this workgroup)
+            blk[slot] = 64u * g < mfix ? 0x07ffffffu - static_cast<uint32_t>(bk[64u * g] >> 32)
+                                       : group_blocks(sorted_len, g);
         }
     }
     __syncthreads();
@@ -1157,7 +1226,20 @@ uint32_t mixed_grid(uint32_t groups, int cus, uint32_t* hcap) {
     return groups;
 }
 
-hipError_t launch_mixed(const BatchArgs& A, const uint32_t* sorted_len, uint32_t* plan, int cus,
+hipError_t launch_plan_layout(const BatchArgs& A, const uint32_t* sorted_len, const BigFix* big, uint32_t* plan,
+                              hipStream_t st) {
+    if (A.n == 0) return hipSuccess;
+    const uint32_t groups = (A.n + 63u) / 64u;
+    // plan area (mixed_plan_bytes): 64 plan words, then the layout summary
+    const uint32_t words = (groups + 31u) / 32u;
+    uint64_t* lay_tb = reinterpret_cast<uint64_t*>(plan + 64);
+    uint32_t* lay_bits = reinterpret_cast<uint32_t*>(lay_tb + words);
+    hipLaunchKernelGGL(plan_layout_kernel, dim3(words), dim3(kLayoutThreads), 0, st, A, sorted_len,
+                       big ? *big : BigFix{}, lay_tb, lay_bits);
+    return hipGetLastError();
+}
+
+hipError_t launch_mixed(const BatchArgs& A, const uint32_t* sorted_len, const BigFix* big, uint32_t* plan, int cus,
                         const int* forced, hipStream_t st) {
     if (A.n == 0) return hipSuccess;
     const uint32_t groups = (A.n + 63u) / 64u;
@@ -1167,8 +1249,10 @@ hipError_t launch_mixed(const BatchArgs& A, const uint32_t* sorted_len, uint32_t
     const uint32_t words = (groups + 31u) / 32u;
     uint64_t* lay_tb = reinterpret_cast<uint64_t*>(plan + 64);
     uint32_t* lay_bits = reinterpret_cast<uint32_t*>(lay_tb + words);
-    if (!forced) hipLaunchKernelGGL(plan_layout_kernel, dim3(words), dim3(kLayoutThreads), 0, st, A, sorted_len,
-                                    lay_tb, lay_bits);
+    if (!forced) {
+        const hipError_t le = launch_plan_layout(A, sorted_len, big, plan, st);
+        if (le != hipSuccess) return le;
+    }
     hipLaunchKernelGGL(plan_mixed_kernel, dim3(1), dim3(kPlanThreads), 0, st, A, sorted_len,
                        (uint32_t)cus, hcap, forced ? 1 : 0, forced ? (uint32_t)forced[0] : 0u,
                        forced ? (uint32_t)forced[1] : 0u, forced ? (uint32_t)forced[2] : 0u, plan, lay_tb,

@@ -404,7 +404,7 @@ bool use_mixed(size_t n, int cus) {
 // 4096)) or H = groups, and F in {4, 8}; or mode 1.
 // SHA1CHUNK_MIXED_DEBUG=1 prints the plan used (synchronises the stream:
 // diagnostics only).
-int launch_mixed_checked(const BatchArgs& A, const uint32_t* sorted_len, uint32_t* plan, int cus,
+int launch_mixed_checked(const BatchArgs& A, const uint32_t* sorted_len, const BigFix* big, uint32_t* plan, int cus,
                          hipStream_t st) {
     if (int rc = check_batch(A)) return rc;
     int forced[3] = {0, 0, 0};
@@ -422,7 +422,7 @@ int launch_mixed_checked(const BatchArgs& A, const uint32_t* sorted_len, uint32_
                         hcap, groups);
         force = true;
     }
-    hipError_t e = launch_mixed(A, sorted_len, plan, cus, force ? forced : nullptr, st);
+    hipError_t e = launch_mixed(A, sorted_len, big, plan, cus, force ? forced : nullptr, st);
     if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "mixed kernel launch: %s", hipGetErrorString(e));
     if (const char* d = getenv("SHA1CHUNK_MIXED_DEBUG"); d && atoi(d)) {
         uint32_t p[28];
@@ -743,10 +743,16 @@ int s1be_hash_device_async(const void* d_base, const uint64_t* d_offsets,
     if (kernel == SHA1CHUNK_KERNEL_AUTO && n > 64) {
         const uint32_t* sorted_len = nullptr;
         uint32_t* plan = nullptr;
-        hipError_t e = sort_by_length_desc(d_lengths, A.n, &A.order, &sorted_len, &plan, &scratch, st);
+        BigFix big{};
+        const bool mixed = use_mixed(n, D->cus);
+        // the mixed path re-ranks chunks of 4 MiB and more exactly (BigFix);
+        // one group per CU or fewer hash all at once, where the grouping of
+        // such chunks cannot change the batch's time
+        hipError_t e = sort_by_length_desc(d_lengths, A.n, &A.order, &sorted_len, &plan, &scratch,
+                                           mixed ? &big : nullptr, st);
         if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "length sort: %s", hipGetErrorString(e));
-        if (use_mixed(n, D->cus)) {
-            rc = launch_mixed_checked(A, sorted_len, plan, D->cus, st);
+        if (mixed) {
+            rc = launch_mixed_checked(A, sorted_len, &big, plan, D->cus, st);
             (void)hipFreeAsync(scratch, st);
             return rc;
         }
@@ -785,13 +791,45 @@ int s1be_sort_order_async(const uint32_t* d_lengths, size_t n, uint32_t* d_order
     const uint32_t *order = nullptr, *sorted_len = nullptr;
     uint32_t* plan = nullptr;
     void* scratch = nullptr;
-    hipError_t e = sort_by_length_desc(d_lengths, static_cast<uint32_t>(n), &order, &sorted_len, &plan, &scratch, st);
+    hipError_t e = sort_by_length_desc(d_lengths, static_cast<uint32_t>(n), &order, &sorted_len, &plan, &scratch,
+                                       nullptr, st);
     if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "length sort: %s", hipGetErrorString(e));
     (void)sorted_len;  // group heads only: every position's length is gathered below
     e = hipMemcpyAsync(d_order, order, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
     if (e == hipSuccess) e = gather_sorted_lengths(d_lengths, order, d_sorted_len, static_cast<uint32_t>(n), st);
     (void)hipFreeAsync(scratch, st);
     if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "sort copy: %s", hipGetErrorString(e));
+    return SHA1CHUNK_OK;
+}
+
+// Diagnostics (tests): the order the mixed path hashes a ragged batch in --
+// the length sort, then the layout kernel's exact re-ranking of chunks of
+// 4 MiB and more (BigFix) -- and the lengths in that order.  d_offsets: the
+// batch's offsets (the layout summary reads them; no bytes are read).
+int s1be_mixed_order_async(const uint32_t* d_lengths, const uint64_t* d_offsets, size_t n, uint32_t* d_order,
+                           uint32_t* d_sorted_len, void* stream) {
+    if (n > 0xffffffffu) return fail(SHA1CHUNK_EINVAL, "n too large");
+    if (n == 0) return SHA1CHUNK_OK;
+    if (!d_lengths || !d_offsets || !d_order || !d_sorted_len) return fail(SHA1CHUNK_EINVAL, "null device pointer");
+    Device* D;
+    if (int rc = get_device(&D)) return rc;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    BatchArgs A{};
+    A.base = reinterpret_cast<const uint8_t*>(d_offsets);  // addresses only, never read
+    A.off = d_offsets;
+    A.len = d_lengths;
+    A.n = static_cast<uint32_t>(n);
+    const uint32_t* sorted_len = nullptr;
+    uint32_t* plan = nullptr;
+    void* scratch = nullptr;
+    BigFix big{};
+    hipError_t e = sort_by_length_desc(d_lengths, A.n, &A.order, &sorted_len, &plan, &scratch, &big, st);
+    if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "length sort: %s", hipGetErrorString(e));
+    e = launch_plan_layout(A, sorted_len, &big, plan, st);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_order, A.order, n * sizeof(uint32_t), hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess) e = gather_sorted_lengths(d_lengths, A.order, d_sorted_len, A.n, st);
+    (void)hipFreeAsync(scratch, st);
+    if (e != hipSuccess) return fail(SHA1CHUNK_EHIP, "mixed order: %s", hipGetErrorString(e));
     return SHA1CHUNK_OK;
 }
 

@@ -82,12 +82,16 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 // (writing the keys), PASS 2 from the first scatter's keys.  One LDS atomic
 // per run of equal slots in a wave (a tile of equal keys otherwise
 // serialises 4096 atomics on one bin).
+// PASS 1 also counts the tile's chunks whose key clamped (big_cnt, if set).
 template <int PASS>
 __global__ __launch_bounds__(kSortThreads) void sort_hist(const uint32_t* len, const uint16_t* keys_in,
-                                                          uint16_t* keys_out, uint32_t* hist, uint32_t n) {
+                                                          uint16_t* keys_out, uint32_t* hist, uint32_t n,
+                                                          uint32_t* big_cnt) {
     __shared__ uint32_t h[256];
+    __shared__ uint32_t nbig;
     const uint32_t tid = threadIdx.x;
     if (tid < 256u) h[tid] = 0u;
+    if (tid == 0u) nbig = 0u;
     __syncthreads();
     const uint32_t base = blockIdx.x * kSortTile;
 #pragma unroll
@@ -106,9 +110,14 @@ __global__ __launch_bounds__(kSortThreads) void sort_hist(const uint32_t* len, c
         const uint32_t s = key_slot<PASS>(k);
         const uint64_t m = slot_peers(valid, s);
         if (valid && lanes_below(m) == 0u) atomicAdd(&h[s], (uint32_t)__popcll(m));
+        if constexpr (PASS == 1) {
+            const uint64_t big = __ballot(valid && k == 0xffffu);
+            if (big && (tid & 63u) == 0u) atomicAdd(&nbig, (uint32_t)__popcll(big));
+        }
     }
     __syncthreads();
     if (tid < 256u) hist[blockIdx.x * 256u + tid] = h[tid];
+    if (PASS == 1 && big_cnt && tid == 0u) big_cnt[blockIdx.x] = nbig;
 }
 
 // Batches of more than kSortMaxTiles tiles: slot blockIdx.x's count in the
@@ -151,7 +160,8 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint16_t* key
                                                              const uint32_t* hist, uint32_t tiles, uint32_t n,
                                                              uint16_t* keys_out, uint32_t* ids_out,
                                                              const uint32_t* len, uint32_t* sorted_len,
-                                                             const uint32_t* pre_in, const uint32_t* tot_in) {
+                                                             const uint32_t* pre_in, const uint32_t* tot_in,
+                                                             uint32_t* big_len, uint32_t* big_id) {
     __shared__ uint32_t start[256];                   // the tile's first position per slot
     __shared__ uint32_t part_tot[4][256], part_pre[4][256], wsum[4];
     __shared__ uint16_t cnt[kSortSlices][256];        // per (item, wave) slice, then its prefix
@@ -262,6 +272,12 @@ __global__ __launch_bounds__(kSortThreads) void sort_scatter(const uint16_t* key
                 // the planner reads a group's first length only (group_blocks):
                 // one gather in 64, not every chunk's
                 if ((dst & 63u) == 0u) sorted_len[dst] = len[id[it]];
+                // a clamped key (>= 65535 blocks) lands in [0, m) in caller
+                // order: its length and id for the exact re-ranking (BigFix)
+                if (big_len && k == 0xffffu && dst < kBigExact) {
+                    big_len[dst] = len[id[it]];
+                    big_id[dst] = id[it];
+                }
             }
         }
     }
@@ -274,7 +290,7 @@ __global__ void gather_lengths(const uint32_t* len, const uint32_t* order, uint3
 }
 
 hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t** d_order,
-                               const uint32_t** d_sorted_len, uint32_t** d_plan, void** scratch,
+                               const uint32_t** d_sorted_len, uint32_t** d_plan, void** scratch, BigFix* big,
                                hipStream_t st) {
     *d_order = nullptr;
     *d_sorted_len = nullptr;
@@ -284,8 +300,11 @@ hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t
     const bool scan = tiles > kSortMaxTiles;  // starts from hist_scan, not summed per workgroup
     const size_t hb = align256(size_t(tiles) * 256u * sizeof(uint32_t));
     const size_t tb = align256(256u * sizeof(uint32_t));
-    // temporaries: hist1, hist2, ids2 [, pre1, pre2, tot1, tot2]
-    const size_t temp_bytes = 2 * hb + align256(size_t(n) * sizeof(uint32_t)) + (scan ? 2 * hb + 2 * tb : 0);
+    // temporaries: hist1, hist2, ids2 [, pre1, pre2, tot1, tot2] [, big_cnt, big_len, big_id]
+    const size_t bigb = big ? align256(size_t(tiles) * sizeof(uint32_t)) + 2 * align256(kBigExact * sizeof(uint32_t))
+                            : 0;
+    const size_t temp_bytes =
+        2 * hb + align256(size_t(n) * sizeof(uint32_t)) + (scan ? 2 * hb + 2 * tb : 0) + bigb;
     // [sorted lengths][order][plan][keys][keys'][temporaries]
     const size_t arr = align256(size_t(n) * sizeof(uint32_t));
     const size_t arr16 = align256(size_t(n) * sizeof(uint16_t));
@@ -308,16 +327,21 @@ hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t
     uint32_t* pre2 = scan ? reinterpret_cast<uint32_t*>(extra + hb) : nullptr;
     uint32_t* tot1 = scan ? reinterpret_cast<uint32_t*>(extra + 2 * hb) : nullptr;
     uint32_t* tot2 = scan ? reinterpret_cast<uint32_t*>(extra + 2 * hb + tb) : nullptr;
+    uint8_t* bigm = extra + (scan ? 2 * hb + 2 * tb : 0);
+    uint32_t* big_cnt = big ? reinterpret_cast<uint32_t*>(bigm) : nullptr;
+    uint32_t* big_len = big ? reinterpret_cast<uint32_t*>(bigm + align256(size_t(tiles) * sizeof(uint32_t))) : nullptr;
+    uint32_t* big_id = big ? big_len + align256(kBigExact * sizeof(uint32_t)) / sizeof(uint32_t) : nullptr;
     hipLaunchKernelGGL(sort_hist<1>, dim3(tiles), dim3(kSortThreads), 0, st, d_len, (const uint16_t*)nullptr, keys,
-                       hist1, n);
+                       hist1, n, big_cnt);
     if (scan) hipLaunchKernelGGL(hist_scan, dim3(256), dim3(kScanThreads), 0, st, hist1, tiles, pre1, tot1);
     hipLaunchKernelGGL(sort_scatter<1>, dim3(tiles), dim3(kSortThreads), 0, st, keys, (const uint32_t*)nullptr, hist1,
-                       tiles, n, keys2, ids2, (const uint32_t*)nullptr, (uint32_t*)nullptr, pre1, tot1);
+                       tiles, n, keys2, ids2, (const uint32_t*)nullptr, (uint32_t*)nullptr, pre1, tot1,
+                       (uint32_t*)nullptr, (uint32_t*)nullptr);
     hipLaunchKernelGGL(sort_hist<2>, dim3(tiles), dim3(kSortThreads), 0, st, (const uint32_t*)nullptr, keys2,
-                       (uint16_t*)nullptr, hist2, n);
+                       (uint16_t*)nullptr, hist2, n, (uint32_t*)nullptr);
     if (scan) hipLaunchKernelGGL(hist_scan, dim3(256), dim3(kScanThreads), 0, st, hist2, tiles, pre2, tot2);
     hipLaunchKernelGGL(sort_scatter<2>, dim3(tiles), dim3(kSortThreads), 0, st, keys2, ids2, hist2, tiles, n,
-                       (uint16_t*)nullptr, order, d_len, sorted_len, pre2, tot2);
+                       (uint16_t*)nullptr, order, d_len, sorted_len, pre2, tot2, big_len, big_id);
     e = hipGetLastError();
     if (e != hipSuccess) {
         (void)hipFreeAsync(mem, st);
@@ -326,6 +350,7 @@ hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t
     *d_order = order;
     *d_sorted_len = sorted_len;
     *d_plan = plan;
+    if (big) *big = BigFix{big_cnt, tiles, big_len, big_id, order, sorted_len};
     *scratch = mem;
     return hipSuccess;
 }

@@ -181,9 +181,12 @@ def model_plan(lengths, C, simulate=True, offsets=None):
     if offsets is None:
         offsets = np.zeros(lengths.size, np.int64)
         offsets[1:] = np.cumsum((lengths + 63) // 64 * 64)[:-1]
-    # the device's order (sha1_sort.hip): descending block counts, clamped
-    # at 65535, ties in caller order
-    order = np.argsort(-np.minimum((lengths + 9 + 63) // 64, 65535), kind="stable")
+    # the device's order: descending block counts, ties in caller order
+    # (sha1_sort.hip sorts on counts clamped at 65535; the layout kernel
+    # re-ranks up to 4096 clamped chunks exactly, BigFix)
+    blocks = (lengths + 9 + 63) // 64
+    exact = int((blocks >= 65535).sum()) <= 4096
+    order = np.argsort(-(blocks if exact else np.minimum(blocks, 65535)), kind="stable")
     srt = lengths[order]
     B = [int(b) for b in total_blocks(srt[::64])]
     G = len(B)
@@ -474,6 +477,34 @@ def test_mixed_beyond_simulated_group_count(pkg, dev, oracle, cus, monkeypatch, 
     (best, bmode, bH, bF), (B, P, L) = model_plan(lens, cus, offsets=off)
     assert len(B) > SIM_MAX_G
     assert model_makespan(B, cus, mode, H, F, P, L) <= best * (1 + 1e-9), ((mode, H, F), (bmode, bH, bF))
+
+
+def test_mixed_big_chunks_exact_order(pkg, dev, oracle, cus, monkeypatch, capfd, dispatch):
+    """Chunks of 4 MiB and more in a mixed batch (their sort keys clamp at
+    65535 blocks): the layout kernel re-ranks them by exact length before the
+    planner prices the groups, so the device plan is the model's best on the
+    exact order, and every digest matches the oracle.  150 chunks of
+    4-14 MiB (exact-length ties among them) in caller order among ~1.1 x CUs
+    groups of short chunks."""
+    torch = dev
+    rng = np.random.default_rng(4242)
+    G = cus + cus // 8 + 3
+    n = 64 * G - 11
+    lens = rng.integers(0, 20000, n).astype(np.uint32)
+    big = rng.choice(n, 150, replace=False)
+    lens[big] = rng.integers(4 << 20, 14 << 20, 150)
+    lens[big[:6]] = 9 << 20
+    off = np.zeros(n, np.uint64)
+    off[1:] = np.cumsum((lens.astype(np.uint64) + 63) // 64 * 64)[: n - 1]
+    host = rng.integers(0, 256, int(off[-1] + lens[-1]) + 64, dtype=np.uint8)
+    want = oracle.hash_batch(host, off, lens)
+    got = run(pkg, torch, host, off, lens, {"SHA1CHUNK_MIXED_DEBUG": "1"}, monkeypatch)
+    _check(got, want, "big chunks, device plan")
+    mode, H, F = _device_plan(capfd)
+    (best, bmode, bH, bF), (B, P, L) = model_plan(lens, cus, offsets=off)
+    assert B[0] == total_blocks(np.array([lens.max()]))[0]  # the heaviest group first, exactly priced
+    got_t = float(sim_plan(B, cus, mode, H, F, L))
+    assert got_t <= best * (1 + 1e-6), ((mode, H, F), got_t, (bmode, bH, bF), best)
 
 
 def test_mixed_config5_law_at_4x(pkg, dev, oracle, cus, monkeypatch, dispatch):

@@ -3,7 +3,9 @@ descending SHA-1 block counts, ceil((len + 9) / 64) clamped at 65535, ties
 in caller order -- numpy's stable argsort of the same keys, position for
 position, and the sorted lengths the planner reads.  Tile edges of the
 three-kernel radix sort (4096 chunks), all-equal and all-distinct keys,
-empty chunks, chunks of 4 MiB and more (clamped keys tie), and the scanned
+empty chunks, chunks of 4 MiB and more (clamped keys tie in the sort; the
+mixed path then re-ranks up to 4096 of them exactly: s1be_mixed_order_async),
+and the scanned
 path beyond 1 Mi chunks (hist_scan starts instead of per-workgroup column
 sums; rocPRIM's onesweep before round 6).  Through the backend's diagnostics
 entry point s1be_sort_order_async (no frontend symbol)."""
@@ -97,6 +99,65 @@ def test_scan_path_beyond_1mi(sort_order, n):
         lens[rng.choice(n, 500, replace=False)] = 0
     lens[rng.choice(n, 1000, replace=False)] = 1 << 23
     check(sort_order, lens)
+
+
+@pytest.fixture(scope="module")
+def mixed_order(pkg, sort_order):
+    """s1be_mixed_order_async: the sort, then the layout kernel's exact
+    re-ranking of chunks of 4 MiB and more (BigFix) -- the order the mixed
+    path hashes in."""
+    import torch
+    be = C.CDLL(os.path.join(PKG_DIR, "libsha1chunk_hip.so"))
+    f = be.s1be_mixed_order_async
+    f.restype = C.c_int
+    f.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p, C.c_void_p, C.c_void_p]
+
+    def run(lens):
+        n = lens.size
+        off = np.zeros(n, np.int64)
+        off[1:] = np.cumsum(lens.astype(np.int64))[:-1]
+        d_len = torch.from_numpy(lens.astype(np.int32)).cuda()
+        d_off = torch.from_numpy(off).cuda()
+        d_ord = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        d_srt = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+        torch.cuda.synchronize()
+        rc = f(d_len.data_ptr(), d_off.data_ptr(), n, d_ord.data_ptr(), d_srt.data_ptr(), None)
+        assert rc == 0, rc
+        torch.cuda.synchronize()
+        return d_ord.cpu().numpy().view(np.uint32), d_srt.cpu().numpy().view(np.uint32)
+
+    return run
+
+
+def exact_keys(lens):
+    return (lens.astype(np.int64) + 9 + 63) // 64
+
+
+@pytest.mark.parametrize("nbig", [0, 1, 100, 2047, 2049, 4096, 4097, 4200])
+def test_mixed_order_exact_for_big_chunks(mixed_order, nbig):
+    """Chunks of 4 MiB and more tie at the clamped sort key; the mixed path
+    re-ranks up to 4096 of them by their exact block counts (stable), across
+    the layout kernel's first two workgroups' positions (2048 each).  Beyond
+    4096 they keep the sort's order (caller order among themselves).  Lengths
+    near the clamp edge (65534..65536 blocks) and equal exact lengths (ties
+    in caller order) included."""
+    rng = np.random.default_rng(nbig + 3)
+    n = 70000
+    lens = rng.integers(0, 1 << 20, n).astype(np.uint64)
+    big = rng.choice(n, nbig, replace=False)
+    lens[big] = rng.integers(65534 * 64 - 9, 1 << 27, nbig)
+    if nbig >= 100:
+        lens[big[:20]] = 5 << 20  # ties
+        lens[big[20:23]] = [65534 * 64 - 9, 65535 * 64 - 9, 65536 * 64 - 9]  # 65534, 65535, 65536 blocks
+    lens = lens.astype(np.uint32)
+    order, srt = mixed_order(lens)
+    # re-ranked when at most 4096 keys clamp (4097: one of them is the
+    # 65534-block chunk, so exactly 4096 clamp; 4200: beyond, caller order)
+    exact = int((exact_keys(lens) >= 65535).sum()) <= 4096
+    w = np.argsort(-(exact_keys(lens) if exact else keys(lens)), kind="stable").astype(np.uint32)
+    bad = np.flatnonzero(order != w)
+    assert bad.size == 0, (nbig, bad[:8], order[bad[:8]], w[bad[:8]])
+    assert np.array_equal(srt, lens[w])
 
 
 @pytest.mark.parametrize("pattern", ["sawtooth", "tile_runs", "alternating", "one_long"])
