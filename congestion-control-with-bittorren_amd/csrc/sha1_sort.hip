@@ -8,9 +8,13 @@
 // of equal block counts keep caller order, so the order is a function of
 // the lengths alone.
 //
-// Keys are 16-bit block counts, ceil((len + 9) / 64) clamped at 65535
-// (chunks of 4 MiB and more tie at the top in caller order; the planner then
-// prices such a group by its first chunk, the hashing is unaffected).
+// Keys are 16-bit block counts, ceil((len + 9) / 64) clamped at 65535:
+// chunks of 4 MiB and more tie at the top in caller order.  For the mixed
+// path the sort also records them (per-tile counts, their lengths and ids,
+// BigFix) and the layout kernel re-ranks up to kBigExact of them by exact
+// block count before the planner prices the groups (round 6, no extra
+// launch); beyond that they stay in caller order.  The hashing is
+// unaffected either way.
 //
 // An LSD radix sort of two 8-bit digits in four launches of its own:
 //   sort_hist<1>     keys, and each tile's low-digit histogram
