@@ -282,6 +282,7 @@ int main(int argc, char **argv) {
     const char *golden_path = "tests/golden/synth_4096x512k.bin";
     const char *mode = "reserve";
     const char *pin = "none";
+    int reps = 1;
     size_t batch = 64;
     B.n = 16384;
     B.distinct = 256;
@@ -296,6 +297,7 @@ int main(int argc, char **argv) {
         else if (!strcmp(argv[i], "--pieces")) B.pieces = atoi(argv[i + 1]);
         else if (!strcmp(argv[i], "--golden")) golden_path = argv[i + 1];
         else if (!strcmp(argv[i], "--pin")) pin = argv[i + 1];
+        else if (!strcmp(argv[i], "--reps")) reps = atoi(argv[i + 1]);
         else {
             fprintf(stderr, "unknown option %s\n", argv[i]);
             return 2;
@@ -320,6 +322,7 @@ int main(int argc, char **argv) {
     B.pin = !strcmp(pin, "gpu") && ncpu_pin > 0;
     /* producer t reads chunks c = t mod threads only when threads divides distinct */
     B.local_src = B.pin && B.distinct % (size_t)B.threads == 0;
+    const char *src_touch = B.local_src ? "producers" : "main thread";
     B.src = (uint8_t *)malloc(B.distinct * (size_t)L512);
     if (!B.local_src)
         for (size_t c = 0; c < B.distinct; ++c) synth_chunk(B.src + c * (size_t)L512, c);
@@ -364,56 +367,68 @@ int main(int argc, char **argv) {
         free(pg);
     }
     if (getenv("VQ_ZC_TRACE")) fprintf(stderr, "vq_zc_bench: ring walked\n");
-    pthread_barrier_init(&B.start, NULL, (unsigned)B.threads + 1);
-    pthread_t *th = (pthread_t *)calloc((size_t)B.threads, sizeof *th);
-    for (int t = 0; t < B.threads; ++t) pthread_create(&th[t], NULL, producer, (void *)(intptr_t)t);
-    struct timespec t0, t1, t2;
-    long long thr0, thr_us0, thr1, thr_us1;
-    pthread_barrier_wait(&B.start);
-    cg_throttle(&thr0, &thr_us0);
-    clock_gettime(CLOCK_MONOTONIC, &t0);
-    for (int t = 0; t < B.threads; ++t) pthread_join(th[t], NULL);
-    clock_gettime(CLOCK_MONOTONIC, &t1);
-    if (getenv("VQ_ZC_TRACE")) fprintf(stderr, "vq_zc_bench: producers joined\n");
-    while (drain(1) > 0) {
-    }
-    clock_gettime(CLOCK_MONOTONIC, &t2);
-    cg_throttle(&thr1, &thr_us1);
-    const double produce = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
-    const double total = (double)(t2.tv_sec - t0.tv_sec) + 1e-9 * (double)(t2.tv_nsec - t0.tv_nsec);
-    size_t right = 0, flagged = 0;
-    for (size_t i = 0; i < B.n; ++i) {
-        const uint8_t want = i % 5 == 2 ? 2 : 1;
-        right += B.result[i] == want;
-        flagged += B.result[i] == 2;
-    }
-    const double gib = (double)B.n * L512 / (double)(1ull << 30);
-    long src_h[MAXNODE + 1] = {0};
-    range_hist(B.src, B.distinct * (size_t)L512, 65536, src_h);
-    printf("{\"mode\": \"%s\", \"producers\": %d, \"chunks\": %zu, \"batch\": %zu, \"pieces\": %d, "
-           "\"seconds\": %.4f, \"produce_seconds\": %.4f, \"GiBps\": %.2f, \"flagged\": %zu, "
-           "\"results_correct\": %s, \"errors\": %d, \"ring_mem\": \"%s\", ",
-           mode, B.threads, B.n, batch, B.pieces, total, produce, gib / total, flagged,
-           right == B.n && !B.errors ? "true" : "false", B.errors,
-           getenv("SHA1CHUNK_VQ_RING_MEM") ? getenv("SHA1CHUNK_VQ_RING_MEM") : "uncached");
-    printf("\"placement\": {\"pin\": \"%s\", \"numa_env\": \"%s\", \"gpu_bdf\": \"%s\", \"gpu_node\": %d, "
-           "\"gpu_node_cpus_allowed\": %d, \"src_first_touch\": \"%s\", \"producers\": [",
-           B.pin ? "gpu" : "none", getenv("SHA1CHUNK_NUMA") ? getenv("SHA1CHUNK_NUMA") : "default", bdf, gnode,
-           ncpu_pin, B.local_src ? "producers" : "main thread");
-    for (int t = 0; t < B.threads && t < 64; ++t)
-        printf("%s{\"cpu_start\": %d, \"node_start\": %d, \"cpu_end\": %d, \"node_end\": %d%s", t ? ", " : "",
-               B.cpu0[t], cpu_node(B.cpu0[t]), B.cpu1[t], cpu_node(B.cpu1[t]), "}");
-    printf("], ");
-    if (B.mode == 1) {
-        printf("\"submit_buffer_nodes\": [");
-        for (int t = 0; t < B.threads && t < 64; ++t) printf("%s%d", t ? ", " : "", B.own_node[t]);
+    int all_right = 1;
+    /* --reps R: R timed passes in this process (fresh producer threads each,
+     * the queue, ring and source chunks reused), one JSON line each */
+    for (int rep = 0; rep < (reps < 1 ? 1 : reps); ++rep) {
+        memset((void *)B.result, 0, B.n);
+        memset(B.bufp, 0, B.n * sizeof *B.bufp);
+        B.local_src = B.local_src && rep == 0; /* the producers' first touch happens once */
+        pthread_barrier_init(&B.start, NULL, (unsigned)B.threads + 1);
+        pthread_t *th = (pthread_t *)calloc((size_t)B.threads, sizeof *th);
+        for (int t = 0; t < B.threads; ++t) pthread_create(&th[t], NULL, producer, (void *)(intptr_t)t);
+        struct timespec t0, t1, t2;
+        long long thr0, thr_us0, thr1, thr_us1;
+        pthread_barrier_wait(&B.start);
+        cg_throttle(&thr0, &thr_us0);
+        clock_gettime(CLOCK_MONOTONIC, &t0);
+        for (int t = 0; t < B.threads; ++t) pthread_join(th[t], NULL);
+        clock_gettime(CLOCK_MONOTONIC, &t1);
+        if (getenv("VQ_ZC_TRACE")) fprintf(stderr, "vq_zc_bench: producers joined\n");
+        while (drain(1) > 0) {
+        }
+        clock_gettime(CLOCK_MONOTONIC, &t2);
+        cg_throttle(&thr1, &thr_us1);
+        free(th);
+        pthread_barrier_destroy(&B.start);
+        const double produce = (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+        const double total = (double)(t2.tv_sec - t0.tv_sec) + 1e-9 * (double)(t2.tv_nsec - t0.tv_nsec);
+        size_t right = 0, flagged = 0;
+        for (size_t i = 0; i < B.n; ++i) {
+            const uint8_t want = i % 5 == 2 ? 2 : 1;
+            right += B.result[i] == want;
+            flagged += B.result[i] == 2;
+        }
+        all_right &= right == B.n && !B.errors;
+        const double gib = (double)B.n * L512 / (double)(1ull << 30);
+        long src_h[MAXNODE + 1] = {0};
+        range_hist(B.src, B.distinct * (size_t)L512, 65536, src_h);
+        printf("{\"mode\": \"%s\", \"rep\": %d, \"producers\": %d, \"chunks\": %zu, \"batch\": %zu, \"pieces\": %d, "
+               "\"seconds\": %.4f, \"produce_seconds\": %.4f, \"GiBps\": %.2f, \"flagged\": %zu, "
+               "\"results_correct\": %s, \"errors\": %d, \"ring_mem\": \"%s\", ",
+               mode, rep, B.threads, B.n, batch, B.pieces, total, produce, gib / total, flagged,
+               right == B.n && !B.errors ? "true" : "false", B.errors,
+               getenv("SHA1CHUNK_VQ_RING_MEM") ? getenv("SHA1CHUNK_VQ_RING_MEM") : "uncached");
+        printf("\"placement\": {\"pin\": \"%s\", \"numa_env\": \"%s\", \"gpu_bdf\": \"%s\", \"gpu_node\": %d, "
+               "\"gpu_node_cpus_allowed\": %d, \"src_first_touch\": \"%s\", \"producers\": [",
+               B.pin ? "gpu" : "none", getenv("SHA1CHUNK_NUMA") ? getenv("SHA1CHUNK_NUMA") : "default", bdf, gnode,
+               ncpu_pin, src_touch);
+        for (int t = 0; t < B.threads && t < 64; ++t)
+            printf("%s{\"cpu_start\": %d, \"node_start\": %d, \"cpu_end\": %d, \"node_end\": %d}", t ? ", " : "",
+                   B.cpu0[t], cpu_node(B.cpu0[t]), B.cpu1[t], cpu_node(B.cpu1[t]));
         printf("], ");
+        if (B.mode == 1) {
+            printf("\"submit_buffer_nodes\": [");
+            for (int t = 0; t < B.threads && t < 64; ++t) printf("%s%d", t ? ", " : "", B.own_node[t]);
+            printf("], ");
+        }
+        put_hist(stdout, "ring_pages", ring_h);
+        printf(", ");
+        put_hist(stdout, "src_pages", src_h);
+        printf(", \"cgroup_nr_throttled\": %lld, \"cgroup_throttled_usec\": %lld}}\n",
+               thr0 >= 0 && thr1 >= 0 ? thr1 - thr0 : -1, thr_us0 >= 0 && thr_us1 >= 0 ? thr_us1 - thr_us0 : -1);
+        fflush(stdout);
     }
-    put_hist(stdout, "ring_pages", ring_h);
-    printf(", ");
-    put_hist(stdout, "src_pages", src_h);
-    printf(", \"cgroup_nr_throttled\": %lld, \"cgroup_throttled_usec\": %lld}}\n",
-           thr0 >= 0 && thr1 >= 0 ? thr1 - thr0 : -1, thr_us0 >= 0 && thr_us1 >= 0 ? thr_us1 - thr_us0 : -1);
     sha1chunk_vq_destroy(B.q);
-    return right == B.n && !B.errors ? 0 : 1;
+    return all_right ? 0 : 1;
 }
