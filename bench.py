@@ -858,64 +858,69 @@ def _config3_leg(pkg, torch, golden, reps: int = 2) -> dict:
             "parity_ref": "digest-of-digests == golden config3.agg (reference sha.c)"}
 
 
-def _verify_queue_leg(h2d_gibps, runs: int = 3) -> dict:
+def _verify_queue_leg(h2d_gibps, reps: int = 5) -> dict:
     """SURVEY 8(f) rank 2, the received-chunk verify queue (reliable_udp.c:121
     session buffer, filled at :339; packet_handler.c:472 -> job.c:217-228):
     16384 x 512 KiB host chunks, reassembled by 4 receive threads in 1484-byte
     DATA payloads, 20 % corrupted in place before the verify, through
     tools/vq_zc_bench (C, linked against libsha1chunk.so): zero-copy
-    (sha1chunk_vq_reserve / commit / release) and the reference's own call
-    shape (fill a malloc'd session buffer, sha1chunk_vq_submit).  The receive
-    threads run on the GPU's NUMA node (--pin gpu: a NIC-local receive path;
-    the library's helper threads are placed there by default, SHA1CHUNK_NUMA)
-    and every run records where its threads and pages were and the cgroup's
-    CPU throttling.  `runs` runs per mode, interleaved: the median is the
-    reported GiB/s, min and max beside it.  Every result is checked against
-    the verdict the reference golden digests give
-    (tests/golden/synth_4096x512k.bin); GiB/s next to this run's pinned H2D."""
+    (sha1chunk_vq_reserve / commit / release), the reference's own call
+    shape (fill a malloc'd session buffer, sha1chunk_vq_submit), and the
+    receive threads' fills alone (reserve, fill, release: no verify) as the
+    bound both sit under.  The receive threads run on the GPU's NUMA node
+    (--pin gpu: a NIC-local receive path; the library's helper threads are
+    placed there by default, SHA1CHUNK_NUMA) and every pass records where its
+    threads and pages were and the cgroup's CPU throttling.  One process per
+    mode, `reps` passes each (--reps): the median pass is the reported GiB/s,
+    min, max and every pass beside it -- single passes swing +-15 % with the
+    host's memory traffic, the fills alone as much (profiles/vq_reps_r06a.jsonl).
+    Every result is checked against the verdict the reference golden digests
+    give (tests/golden/synth_4096x512k.bin); GiB/s next to this run's pinned
+    H2D."""
     import subprocess
     tool = os.path.join(ROOT, "tools", "vq_zc_bench")
     out = {"workload": "16384 x 524288 B host chunks, 4 receive threads filling 1484-byte pieces, "
-                       "20 % corrupted, persistent drain", "pinned_h2d_GiBps": h2d_gibps, "runs_per_mode": runs}
+                       "20 % corrupted, persistent drain", "pinned_h2d_GiBps": h2d_gibps, "passes_per_mode": reps}
     if not os.path.exists(tool):
         out["error"] = "tools/vq_zc_bench not built (make -C congestion-control-with-bittorren_amd tools)"
         return out
-    recs = {"reserve": [], "submit": []}
-    for _ in range(runs):
-        for mode in ("reserve", "submit"):
-            try:
-                r = subprocess.run([tool, "--mode", mode, "--chunks", "16384", "--producers", "4",
-                                    "--distinct", "4096", "--pieces", "1", "--pin", "gpu",
-                                    "--golden", os.path.join(ROOT, "tests/golden/synth_4096x512k.bin")],
-                                   capture_output=True, text=True, timeout=180, cwd=ROOT)
-                line = [x for x in r.stdout.splitlines() if x.startswith("{")]
-                rec = json.loads(line[-1]) if line else {"error": (r.stderr or r.stdout)[-300:]}
-            except Exception as e:  # a failed run must not cost the bench line
-                rec = {"error": repr(e)[:300]}
-            recs[mode].append(rec)
-    for mode, key in (("reserve", "zero_copy"), ("submit", "submit")):
-        rs = recs[mode]
-        good = [r for r in rs if "GiBps" in r]
-        if not good:
-            out[key] = {"error": rs[-1].get("error") if rs else "no run"}
+    for mode, key in (("fill", "fill_only"), ("reserve", "zero_copy"), ("submit", "submit")):
+        try:
+            r = subprocess.run([tool, "--mode", mode, "--chunks", "16384", "--producers", "4",
+                                "--distinct", "4096", "--pieces", "1", "--pin", "gpu", "--reps", str(reps),
+                                "--golden", os.path.join(ROOT, "tests/golden/synth_4096x512k.bin")],
+                               capture_output=True, text=True, timeout=180, cwd=ROOT)
+            good = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
+            if r.returncode != 0 or len(good) != reps:
+                out[key] = {"error": f"rc {r.returncode}, {len(good)} passes: {(r.stderr or r.stdout)[-300:]}"}
+                continue
+        except Exception as e:  # a failed mode must not cost the bench line
+            out[key] = {"error": repr(e)[:300]}
             continue
-        rates = [r["GiBps"] for r in good]
+        rates = [g["GiBps"] for g in good]
         med = good[int(np.argsort(rates)[len(rates) // 2])]
         rec = dict(med)
         rec["GiBps"] = float(np.median(rates))
-        rec["GiBps_runs"] = rates
+        rec["GiBps_passes"] = rates
         rec["GiBps_min"], rec["GiBps_max"] = min(rates), max(rates)
         rec["spread"] = round((max(rates) - min(rates)) / rec["GiBps"], 4)
-        rec["produce_seconds_runs"] = [r["produce_seconds"] for r in good]
-        rec["placement_runs"] = [{"producer_nodes": sorted({p["node_end"] for p in r["placement"]["producers"]}),
-                                  "cgroup_nr_throttled": r["placement"]["cgroup_nr_throttled"]} for r in good]
-        rec["parity"] = len(good) == len(rs) and all(
-            bool(r.get("results_correct")) and r.get("flagged") == len(range(2, 16384, 5)) for r in good)
+        rec["produce_seconds_passes"] = [g["produce_seconds"] for g in good]
+        rec["placement_passes"] = [{"producer_cpus": [q["cpu_start"] for q in g["placement"]["producers"]],
+                                    "producer_nodes": sorted({q["node_end"] for q in g["placement"]["producers"]}),
+                                    "cgroup_nr_throttled": g["placement"]["cgroup_nr_throttled"]} for g in good]
+        if mode != "fill":
+            rec["parity"] = all(bool(g.get("results_correct")) and g.get("flagged") == len(range(2, 16384, 5))
+                                for g in good)
         if h2d_gibps:
             rec["over_h2d"] = round(rec["GiBps"] / h2d_gibps, 4)
         out[key] = rec
+    fill = out.get("fill_only", {}).get("GiBps")
+    for key in ("zero_copy", "submit"):
+        if fill and "GiBps" in out.get(key, {}):
+            out[key]["over_fill_only"] = round(out[key]["GiBps"] / fill, 4)
     out["parity"] = all(out.get(k, {}).get("parity", False) for k in ("zero_copy", "submit"))
-    out["parity_ref"] = "every chunk's 0/1 == (its bytes hash to the reference golden digest); 3277 flagged"
+    out["parity_ref"] = "every chunk's 0/1 == (its bytes hash to the reference golden digest); 3277 flagged, " \
+                        "every pass"
     return out
 
 
