@@ -9,8 +9,8 @@ import json
 import sqlite3
 import sys
 
-PRE = ("sort_keys_hist", "sort_hist", "sort_scatter", "plan_layout_kernel", "plan_mixed_kernel", "block_keys16",
-       "gather_lengths", "rocprim")
+PRE = ("sort_keys_hist", "sort_hist", "sort_scatter", "hist_scan", "plan_layout_tail_kernel", "plan_layout_kernel",
+       "plan_mixed_kernel", "block_keys16", "gather_lengths", "rocprim")
 
 
 def short(name):
