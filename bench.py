@@ -867,13 +867,21 @@ def _verify_queue_leg(h2d_gibps, reps: int = 5) -> dict:
     (sha1chunk_vq_reserve / commit / release), the reference's own call
     shape (fill a malloc'd session buffer, sha1chunk_vq_submit), and the
     receive threads' fills alone (reserve, fill, release: no verify) as the
-    bound both sit under.  The receive threads run on the GPU's NUMA node
+    bound both sit under.  The payload pieces come from 64 distinct source
+    chunks (32 MiB, cache-resident), as a receive path copies each datagram
+    from a just-received packet buffer (peer.c:81 recvfrom ->
+    reliable_udp.c:339 memcpy); zero-copy is timed once more with 4096
+    distinct source chunks (2 GiB read from DRAM), the round-5 shape, whose
+    host memory traffic swings it run to run (profiles/vq_reps_d*.jsonl).
+    The receive threads run on the GPU's NUMA node
     (--pin gpu: a NIC-local receive path; the library's helper threads are
     placed there by default, SHA1CHUNK_NUMA) and every pass records where its
     threads and pages were and the cgroup's CPU throttling.  One process per
     mode, `reps` passes each (--reps): the median pass is the reported GiB/s,
-    min, max and every pass beside it -- single passes swing +-15 % with the
-    host's memory traffic, the fills alone as much (profiles/vq_reps_r06a.jsonl).
+    min, max and every pass beside it -- from the DRAM source single passes
+    swing +-15 % with the host's memory traffic, the fills alone as much
+    (profiles/vq_reps_r06a.jsonl); from the cache-resident one zero-copy
+    passes stay within 6 % (profiles/vq_reps_d64.jsonl).
     Every result is checked against the verdict the reference golden digests
     give (tests/golden/synth_4096x512k.bin); GiB/s next to this run's pinned
     H2D."""
@@ -884,10 +892,13 @@ def _verify_queue_leg(h2d_gibps, reps: int = 5) -> dict:
     if not os.path.exists(tool):
         out["error"] = "tools/vq_zc_bench not built (make -C congestion-control-with-bittorren_amd tools)"
         return out
-    for mode, key in (("fill", "fill_only"), ("reserve", "zero_copy"), ("submit", "submit")):
+    out["source"] = "64 distinct source chunks (32 MiB, cache-resident: the packet buffers a receive path " \
+                    "copies from); zero_copy_dram_source: 4096 (2 GiB)"
+    for mode, key, distinct in (("fill", "fill_only", 64), ("reserve", "zero_copy", 64), ("submit", "submit", 64),
+                                ("reserve", "zero_copy_dram_source", 4096)):
         try:
             r = subprocess.run([tool, "--mode", mode, "--chunks", "16384", "--producers", "4",
-                                "--distinct", "4096", "--pieces", "1", "--pin", "gpu", "--reps", str(reps),
+                                "--distinct", str(distinct), "--pieces", "1", "--pin", "gpu", "--reps", str(reps),
                                 "--golden", os.path.join(ROOT, "tests/golden/synth_4096x512k.bin")],
                                capture_output=True, text=True, timeout=180, cwd=ROOT)
             good = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]
@@ -918,7 +929,7 @@ def _verify_queue_leg(h2d_gibps, reps: int = 5) -> dict:
     for key in ("zero_copy", "submit"):
         if fill and "GiBps" in out.get(key, {}):
             out[key]["over_fill_only"] = round(out[key]["GiBps"] / fill, 4)
-    out["parity"] = all(out.get(k, {}).get("parity", False) for k in ("zero_copy", "submit"))
+    out["parity"] = all(out.get(k, {}).get("parity", False) for k in ("zero_copy", "submit", "zero_copy_dram_source"))
     out["parity_ref"] = "every chunk's 0/1 == (its bytes hash to the reference golden digest); 3277 flagged, " \
                         "every pass"
     return out
