@@ -106,7 +106,7 @@ hipError_t launch_compare(const uint8_t* dig, const uint8_t* exp, uint32_t n, ui
 // consuming kernel has been enqueued.
 inline size_t mixed_plan_bytes(uint32_t n) {
     const size_t words = ((size_t(n) + 63) / 64 + 31) / 32;  // one per 32 groups of 64 chunks
-    return 256 + ((words * 12 + 255) & ~size_t(255));
+    return 256 + ((words * 12 + words * 32 * 4 + 255) & ~size_t(255));  // + a block count per group
 }
 // big (or null): receives the clamped chunks' re-ranking inputs (BigFix).
 hipError_t sort_by_length_desc(const uint32_t* d_len, uint32_t n, const uint32_t** d_order,

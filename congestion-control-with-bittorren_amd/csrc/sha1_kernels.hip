@@ -389,7 +389,8 @@ constexpr uint32_t kLayoutGroupsPerWave = 32 / (kLayoutThreads / 64);
 constexpr uint32_t kLayoutPositions = 32u * 64u;  // positions per layout workgroup
 
 __global__ __launch_bounds__(kLayoutThreads) void plan_layout_kernel(BatchArgs A, const uint32_t* sorted_len,
-                                                                     BigFix B, uint64_t* tb, uint32_t* bits) {
+                                                                     BigFix B, uint64_t* tb, uint32_t* bits,
+                                                                     uint32_t* gblk) {
     const uint32_t lane = threadIdx.x % 64u, wave = threadIdx.x / 64u;
     const uint32_t G = (A.n + 63u) / 64u;
     __shared__ uint32_t tog[32], blk[32];
@@ -409,7 +410,6 @@ __global__ __launch_bounds__(kLayoutThreads) void plan_layout_kernel(BatchArgs A
             en[k].len = 0;
         }
     }
-    uint32_t mfix = 0;  // positions below this were re-ranked here (their heads' blocks in bk)
     // position 0 holds the largest key: below the clamp, no chunk clamped and
     // nothing more to read (one load, in flight with the entries')
     if (B.cnt && blockIdx.x * kLayoutPositions < kBigExact && total_blocks(sorted_len[0]) >= 65535u) {
@@ -460,7 +460,6 @@ __global__ __launch_bounds__(kLayoutThreads) void plan_layout_kernel(BatchArgs A
                     en[k].len = B.len[j];
                 }
             }
-            mfix = m;
         }
     }
 #pragma unroll
@@ -486,10 +485,12 @@ __global__ __launch_bounds__(kLayoutThreads) void plan_layout_kernel(BatchArgs A
         }
         if (lane == 0) {
             tog[slot] = hi - lo <= 2 * bytes + (2ull << 20) ? 1u : 0u;
-            // a re-ranked head's blocks from LDS (its sorted_len was rewritten
-            // just now by this workgroup)
-            blk[slot] = 64u * g < mfix ? 0x07ffffffu - static_cast<uint32_t>(bk[64u * g] >> 32)
-                                       : group_blocks(sorted_len, g);
+            // the head's blocks from its entry (lane 0 holds position 64g: the
+            // length sorted_len[64g] holds, or a re-ranked head's), written
+            // for the planner as one coalesced array
+            const uint32_t b = total_blocks(en[k].len);
+            blk[slot] = b;
+            gblk[g] = b;
         }
     }
     __syncthreads();
@@ -518,12 +519,15 @@ struct PlanLayout {
     }
 };
 
+// Branch-free (a wave's lanes price plans of both modes; the same values
+// as the three-way branch it replaced, which ran each side in turn).
 __device__ __forceinline__ double job_time(const uint32_t* sorted_len, const uint32_t* blocks, const PlanLayout& L,
                                            uint32_t G, uint32_t mode, uint32_t H, uint32_t F, uint32_t i) {
-    if (mode == 1) return plan_blocks(sorted_len, blocks, 2u * i) * kChainSplit8;
-    if (i < H) return plan_blocks(sorted_len, blocks, i) * kChainSplit4;
-    const uint32_t g = H + (i - H) * F;
-    return plan_blocks(sorted_len, blocks, g) * fused_chain(F, L.job_together(g, F, G));
+    const bool split = mode == 1 || i < H;
+    const uint32_t g = mode == 1 ? 2u * i : (i < H ? i : H + (i - H) * F);
+    const double fc = fused_chain(F, L.job_together(g, F, G));
+    const double c = mode == 1 ? kChainSplit8 : (split ? kChainSplit4 : fc);
+    return plan_blocks(sorted_len, blocks, g) * c;
 }
 
 // Estimated makespan of a plan: the largest of
@@ -550,8 +554,19 @@ __device__ double makespan(const uint32_t* sorted_len, const uint32_t* blocks, c
     }
     double m = fmax(W / C, job_time(sorted_len, blocks, L, G, mode, H, F, 0));
     if (mode == 0 && H > 0 && H < G) m = fmax(m, job_time(sorted_len, blocks, L, G, mode, H, F, H));
-    for (uint32_t k = 1; (uint64_t)k * C < J; ++k)
-        m = fmax(m, (k + 1) * job_time(sorted_len, blocks, L, G, mode, H, F, k * C));
+    // the rounds bound four k at a time, their reads in flight together (a
+    // k past the jobs prices job J - 1 and counts 0; the maximum is the same
+    // in any order: every term is finite and >= 0)
+    for (uint32_t k = 1; (uint64_t)k * C < J; k += 4u) {
+        double v[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4u; ++u) {
+            const uint64_t i = (uint64_t)(k + u) * C;
+            const double t = job_time(sorted_len, blocks, L, G, mode, H, F, i < J ? (uint32_t)i : J - 1u);
+            v[u] = i < J ? (k + u + 1) * t : 0.0;
+        }
+        m = fmax(m, fmax(fmax(v[0], v[1]), fmax(v[2], v[3])));
+    }
     return m;
 }
 
@@ -687,12 +702,16 @@ __device__ __forceinline__ float sim_xcd(const uint32_t* blocks, uint32_t G, uin
 // {fmode, fh, ff} as given (tests, A/B).
 constexpr int kPlanThreads = 1024;
 constexpr uint32_t kPlanMaxH = 4096;  // largest split head the model search considers
+// (H, F) pairs whose bounds the search keeps for the candidates: every pair
+// while the head cap (mixed_grid: min(G, 4 x CUs, 4096)) is <= 1024, as on
+// 256 CUs; the candidates of a larger cap recompute theirs
+constexpr uint32_t kPairStore = 2u * 1025u + 1u;
 
 __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, const uint32_t* sorted_len,
                                                                   uint32_t cus, uint32_t hcap, int forced,
                                                                   uint32_t fmode, uint32_t fh, uint32_t ff,
                                                                   uint32_t* plan, const uint64_t* lay_tb,
-                                                                  const uint32_t* lay_bits) {
+                                                                  const uint32_t* lay_bits, const uint32_t* lay_blk) {
     const uint32_t n = A.n;
     const uint32_t t = threadIdx.x;
     if (t == 0) plan[3] = 0u;  // the persistent kernel's job counter
@@ -725,7 +744,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     __shared__ uint32_t blocks[kSimMaxG];  // group_blocks of groups < kSimMaxG, for the simulation
     __shared__ uint32_t togw[kSimMaxG / 32];  // plan_layout_kernel's bits, groups < kSimMaxG
     for (uint32_t g = g0; g < g1; ++g) {
-        const uint32_t b = group_blocks(sorted_len, g);
+        const uint32_t b = lay_blk[g];  // group_blocks(sorted_len, g), coalesced (plan_layout_kernel)
         if (g < kSimMaxG) blocks[g] = b;
         local += b;
     }
@@ -791,13 +810,18 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     double bm = 1e300;
     uint32_t bh = 0, bf = 4;
     const uint32_t npair = 2u * (hcap + 1u) + (G > hcap ? 1u : 0u);
+    __shared__ double pbnd[kPairStore];  // pair w's bound, for the candidates' (same call, same value)
+    __shared__ double m1b;               // the 8-wave mode's bound
     for (uint32_t w = t; w < npair; w += kPlanThreads) {
         const bool all = w == 2u * (hcap + 1u);  // H = G beyond hcap
         const uint32_t H = all ? G : w / 2u, F = all ? 4u : 4u + 4u * (w & 1u);
         if (F == 8u && H >= G) continue;  // H = G: every group split, F = 4 only
         const double m = makespan(sorted_len, blocks, L, ft, G, cus, 0, H, F, all ? PG : prefix[H], PG);
+        if (w < kPairStore) pbnd[w] = m;
         if (m < bm || (m == bm && (H < bh || (H == bh && F < bf)))) { bm = m; bh = H; bf = F; }
     }
+    // the last thread has the fewest pairs (or as many as any)
+    if (t == kPlanThreads - 1) m1b = makespan(sorted_len, blocks, L, ft, G, cus, 1, 0, 0, 0, PG);
     if (t == 0) bsub[2] = __builtin_amdgcn_s_memtime();
     // the smallest (bound, head, F) over the workgroup: in the wave, then
     // over the 16 waves' bests
@@ -846,7 +870,7 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     const bool simulate = G <= kSimMaxG && cus % kSimXcds == 0 && cus / kSimXcds <= kSimCus;
     if (!simulate) {
         if (t == 0) {
-            const bool split8 = makespan(sorted_len, blocks, L, ft, G, cus, 1, 0, 0, 0, PG) < best_m[0];
+            const bool split8 = m1b < best_m[0];
             plan[0] = split8 ? 1u : 0u;
             plan[1] = split8 ? 0u : best_h[0];
             plan[2] = split8 ? 0u : best_f[0];
@@ -921,10 +945,13 @@ __global__ __launch_bounds__(kPlanThreads) void plan_mixed_kernel(BatchArgs A, c
     __syncthreads();
     uint64_t sub[3] = {0, 0, 0};  // shader-clock stamps inside the first sweep's stage (plan[20..22])
     if (t == 0) sub[0] = __builtin_amdgcn_s_memtime();
-    if (t >= 1 && t < ncand) {
+    if (t >= 1 && t < ncand) {  // the search's bounds (a call costs ~5 k cycles of latency)
         const uint32_t m = cmode[t], h = chead[t], f = cf[t];
-        clb[t] = m == 1 ? makespan(sorted_len, blocks, L, ft, G, cus, 1, 0, 0, 0, PG)
-                        : makespan(sorted_len, blocks, L, ft, G, cus, 0, h, f, h <= hcap ? prefix[h] : PG, PG);
+        const uint32_t w = h <= hcap ? 2u * h + (f == 8u ? 1u : 0u) : 2u * (hcap + 1u);  // its pair
+        clb[t] = m == 1 ? m1b
+                        : (w < kPairStore ? pbnd[w]
+                                          : makespan(sorted_len, blocks, L, ft, G, cus, 0, h, f,
+                                                     h <= hcap ? prefix[h] : PG, PG));
     }
     __syncthreads();
     if (t == 0) sub[1] = __builtin_amdgcn_s_memtime();
@@ -1234,8 +1261,9 @@ hipError_t launch_plan_layout(const BatchArgs& A, const uint32_t* sorted_len, co
     const uint32_t words = (groups + 31u) / 32u;
     uint64_t* lay_tb = reinterpret_cast<uint64_t*>(plan + 64);
     uint32_t* lay_bits = reinterpret_cast<uint32_t*>(lay_tb + words);
+    uint32_t* lay_blk = lay_bits + words;
     hipLaunchKernelGGL(plan_layout_kernel, dim3(words), dim3(kLayoutThreads), 0, st, A, sorted_len,
-                       big ? *big : BigFix{}, lay_tb, lay_bits);
+                       big ? *big : BigFix{}, lay_tb, lay_bits, lay_blk);
     return hipGetLastError();
 }
 
@@ -1249,6 +1277,7 @@ hipError_t launch_mixed(const BatchArgs& A, const uint32_t* sorted_len, const Bi
     const uint32_t words = (groups + 31u) / 32u;
     uint64_t* lay_tb = reinterpret_cast<uint64_t*>(plan + 64);
     uint32_t* lay_bits = reinterpret_cast<uint32_t*>(lay_tb + words);
+    const uint32_t* lay_blk = lay_bits + words;
     if (!forced) {
         const hipError_t le = launch_plan_layout(A, sorted_len, big, plan, st);
         if (le != hipSuccess) return le;
@@ -1256,7 +1285,7 @@ hipError_t launch_mixed(const BatchArgs& A, const uint32_t* sorted_len, const Bi
     hipLaunchKernelGGL(plan_mixed_kernel, dim3(1), dim3(kPlanThreads), 0, st, A, sorted_len,
                        (uint32_t)cus, hcap, forced ? 1 : 0, forced ? (uint32_t)forced[0] : 0u,
                        forced ? (uint32_t)forced[1] : 0u, forced ? (uint32_t)forced[2] : 0u, plan, lay_tb,
-                       lay_bits);
+                       lay_bits, lay_blk);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     BatchArgs B = A;
