@@ -873,10 +873,13 @@ def _verify_queue_leg(h2d_gibps, reps: int = 5) -> dict:
     reliable_udp.c:339 memcpy); zero-copy is timed once more with 4096
     distinct source chunks (2 GiB read from DRAM), the round-5 shape, whose
     host memory traffic swings it run to run (profiles/vq_reps_d*.jsonl).
-    The receive threads run on the GPU's NUMA node
-    (--pin gpu: a NIC-local receive path; the library's helper threads are
-    placed there by default, SHA1CHUNK_NUMA) and every pass records where its
-    threads and pages were and the cgroup's CPU throttling.  One process per
+    The receive threads run on the GPU's NUMA node, one per L3 domain (CCD)
+    of it (--pin l3: a NIC-local receive path with a CCD per thread; left to
+    float over the node, --pin gpu, `submit` passes ranged 25.9-36.2 GiB/s
+    against 27.7-29.6, zero-copy the same either way, profiles/vq_l3.jsonl;
+    the library's helper threads are placed on the node by default,
+    SHA1CHUNK_NUMA) and every pass records where its threads and pages were
+    and the cgroup's CPU throttling.  One process per
     mode, `reps` passes each (--reps): the median pass is the reported GiB/s,
     min, max and every pass beside it -- from the DRAM source single passes
     swing +-15 % with the host's memory traffic, the fills alone as much
@@ -898,7 +901,7 @@ def _verify_queue_leg(h2d_gibps, reps: int = 5) -> dict:
                                 ("reserve", "zero_copy_dram_source", 4096)):
         try:
             r = subprocess.run([tool, "--mode", mode, "--chunks", "16384", "--producers", "4",
-                                "--distinct", str(distinct), "--pieces", "1", "--pin", "gpu", "--reps", str(reps),
+                                "--distinct", str(distinct), "--pieces", "1", "--pin", "l3", "--reps", str(reps),
                                 "--golden", os.path.join(ROOT, "tests/golden/synth_4096x512k.bin")],
                                capture_output=True, text=True, timeout=180, cwd=ROOT)
             good = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")]

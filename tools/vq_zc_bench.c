@@ -30,7 +30,10 @@
  * timed region.  --pin gpu binds every producer to the GPU node's CPUs
  * (within this process's affinity mask) and has each producer write its own
  * source chunks there (first touch), as a NIC-local receive thread would;
- * --pin none leaves placement to the scheduler.
+ * --pin none leaves placement to the scheduler.  --pin l3 binds producer t
+ * to the t-th L3 domain (the CPUs sharing cache/index3) of the GPU node's
+ * CPUs, round robin: one receive thread per CCD, each with its own L3 and
+ * link to the memory controllers.
  */
 #define _GNU_SOURCE
 #include <ctype.h>
@@ -156,6 +159,37 @@ static int node_cpus(int node, cpu_set_t *out) {
     return CPU_COUNT(out);
 }
 
+/* The L3 domains of the CPUs in `within`, in CPU order (at most maxd). */
+static int l3_domains(const cpu_set_t *within, cpu_set_t *dom, int maxd) {
+    int nd = 0;
+    cpu_set_t seen;
+    CPU_ZERO(&seen);
+    for (int c = 0; c < CPU_SETSIZE && nd < maxd; ++c) {
+        if (!CPU_ISSET(c, within) || CPU_ISSET(c, &seen)) continue;
+        char path[128], buf[4096];
+        snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", c);
+        FILE *f = fopen(path, "r");
+        if (!f) return 0;
+        if (!fgets(buf, sizeof buf, f)) buf[0] = 0;
+        fclose(f);
+        CPU_ZERO(&dom[nd]);
+        for (char *tok = strtok(buf, ",\n"); tok; tok = strtok(NULL, ",\n")) {
+            int a, b;
+            const int k = sscanf(tok, "%d-%d", &a, &b);
+            if (k < 1) continue;
+            if (k == 1) b = a;
+            for (int x = a; x <= b && x < CPU_SETSIZE; ++x)
+                if (CPU_ISSET(x, within)) {
+                    CPU_SET(x, &dom[nd]);
+                    CPU_SET(x, &seen);
+                }
+        }
+        CPU_SET(c, &seen);
+        if (CPU_COUNT(&dom[nd]) > 0) ++nd;
+    }
+    return nd;
+}
+
 /* cgroup CPU throttling counters (v2 cpu.stat; v1 cpu/cpu.stat, ns) */
 static void cg_throttle(long long *nr, long long *usec) {
     *nr = *usec = -1;
@@ -190,6 +224,8 @@ static struct {
     int pin;           /* 1: producers on the GPU node's CPUs, source chunks first-touched there */
     int local_src;     /* producers write their own source chunks */
     cpu_set_t pin_set;
+    int ndom;          /* --pin l3: producer t on dom[t % ndom] */
+    cpu_set_t dom[64];
     int cpu0[64], cpu1[64];
     int own_node[64]; /* submit: the node of each producer's session buffer (-1 unknown) */
 } B;
@@ -227,7 +263,7 @@ static void fill(uint8_t *dst, const uint8_t *src) {
 
 static void *producer(void *arg) {
     const int t = (int)(intptr_t)arg;
-    if (B.pin) (void)sched_setaffinity(0, sizeof B.pin_set, &B.pin_set);
+    if (B.pin) (void)sched_setaffinity(0, sizeof B.pin_set, B.ndom ? &B.dom[t % B.ndom] : &B.pin_set);
     if (B.local_src)
         for (size_t c = (size_t)t; c < B.distinct; c += (size_t)B.threads)
             synth_chunk(B.src + c * (size_t)L512, c);
@@ -305,8 +341,8 @@ int main(int argc, char **argv) {
     }
     B.mode = !strcmp(mode, "submit") ? 1 : (!strcmp(mode, "fill") ? 2 : 0);
     if (B.threads < 1 || B.distinct < 1 || B.distinct > 4096) return 2;
-    if (strcmp(pin, "none") && strcmp(pin, "gpu")) {
-        fprintf(stderr, "--pin none|gpu\n");
+    if (strcmp(pin, "none") && strcmp(pin, "gpu") && strcmp(pin, "l3")) {
+        fprintf(stderr, "--pin none|gpu|l3\n");
         return 2;
     }
     B.golden = (uint8_t *)malloc(20 * B.distinct);
@@ -319,7 +355,8 @@ int main(int argc, char **argv) {
     char bdf[64];
     const int gnode = gpu_node(bdf, sizeof bdf);
     const int ncpu_pin = node_cpus(gnode, &B.pin_set);
-    B.pin = !strcmp(pin, "gpu") && ncpu_pin > 0;
+    B.pin = strcmp(pin, "none") && ncpu_pin > 0;
+    B.ndom = B.pin && !strcmp(pin, "l3") ? l3_domains(&B.pin_set, B.dom, 64) : 0;
     /* producer t reads chunks c = t mod threads only when threads divides distinct */
     B.local_src = B.pin && B.distinct % (size_t)B.threads == 0;
     const char *src_touch = B.local_src ? "producers" : "main thread";
@@ -410,9 +447,9 @@ int main(int argc, char **argv) {
                right == B.n && !B.errors ? "true" : "false", B.errors,
                getenv("SHA1CHUNK_VQ_RING_MEM") ? getenv("SHA1CHUNK_VQ_RING_MEM") : "uncached");
         printf("\"placement\": {\"pin\": \"%s\", \"numa_env\": \"%s\", \"gpu_bdf\": \"%s\", \"gpu_node\": %d, "
-               "\"gpu_node_cpus_allowed\": %d, \"src_first_touch\": \"%s\", \"producers\": [",
-               B.pin ? "gpu" : "none", getenv("SHA1CHUNK_NUMA") ? getenv("SHA1CHUNK_NUMA") : "default", bdf, gnode,
-               ncpu_pin, src_touch);
+               "\"gpu_node_cpus_allowed\": %d, \"l3_domains\": %d, \"src_first_touch\": \"%s\", \"producers\": [",
+               B.pin ? (B.ndom ? "l3" : "gpu") : "none", getenv("SHA1CHUNK_NUMA") ? getenv("SHA1CHUNK_NUMA") : "default", bdf, gnode,
+               ncpu_pin, B.ndom, src_touch);
         for (int t = 0; t < B.threads && t < 64; ++t)
             printf("%s{\"cpu_start\": %d, \"node_start\": %d, \"cpu_end\": %d, \"node_end\": %d}", t ? ", " : "",
                    B.cpu0[t], cpu_node(B.cpu0[t]), B.cpu1[t], cpu_node(B.cpu1[t]));
