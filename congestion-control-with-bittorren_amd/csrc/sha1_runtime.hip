@@ -1269,9 +1269,17 @@ constexpr int kVqSets = 3;
 
 int vq_copy_helpers() {
     const char* e = getenv("SHA1CHUNK_VQ_THREADS");
-    // threads in all, the caller included; 4 measured best on the GPU box
-    // (16384 x 512 KiB, batch 1024: 1 / 4 / 8 threads 16.9 / 46.4 / 36.5 GiB/s)
-    return std::max(0, (e ? atoi(e) : 4) - 1);
+    // threads in all, the caller included.  Default 1: the calling thread
+    // copies the chunk it has just filled (hot in its own core's caches);
+    // helper threads on other cores have to pull it across the fabric and
+    // cost more than they add.  16384 x 512 KiB, 1484-byte fills, receive
+    // threads one per L3 domain (profiles/vq_threads*_r06.jsonl): 1 / 4
+    // receive threads at 1 copy thread 18.5 / 46.7 GiB/s, at 4 7.7 / 26.8
+    // (persistent queue; batch mode 19.3 / 29.2 against 8.8 / 22.4, and the
+    // same with a DRAM-resident source).  Round 2 had measured 4 best (16.9
+    // / 46.4 / 36.5 GiB/s for 1 / 4 / 8 on one thread submitting batches of
+    // 1024) on the round-2 queue.
+    return std::max(0, (e ? atoi(e) : 1) - 1);
 }
 
 struct VqSet {

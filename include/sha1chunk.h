@@ -214,12 +214,14 @@ int sha1chunk_synth_fill_ragged_async(void *d_base, const uint64_t *d_offsets,
  * queue.  Persistent drains of all queues on one device hold at most
  * SHA1CHUNK_VQ_CU_BUDGET CUs (default half the device); a queue created
  * when that budget is spent uses batch launches.  The copy of submit() runs
- * on SHA1CHUNK_VQ_THREADS threads (default 4, the caller included: three
- * helper threads per queue that spin briefly between submissions) when no
- * other submit is using them, else on the calling thread; reserve/commit
- * has no copy.  The helper threads run on the CPUs of the GPU's NUMA node
- * (SHA1CHUNK_NUMA=off: anywhere); HIP's pinned allocation puts the ring's
- * pages on that node already (measured, every page).
+ * on the calling thread, which has just filled the chunk and holds it in its
+ * caches (SHA1CHUNK_VQ_THREADS=N > 1 splits it over N threads, the caller
+ * and N - 1 helper threads per queue that spin briefly between submissions,
+ * when no other submit is using them: measured slower, 1 / 4 receive threads
+ * 7.7 / 26.8 GiB/s at N = 4 against 18.5 / 46.7 at the default 1);
+ * reserve/commit has no copy.  Helper threads run on the CPUs of the GPU's
+ * NUMA node (SHA1CHUNK_NUMA=off: anywhere); HIP's pinned allocation puts the
+ * ring's pages on that node already (measured, every page).
  * Measured on 16384 x 512 KiB host chunks from 4 receive threads on the
  * GPU's node, pieces copied from a cache-resident source: 44-47 GiB/s
  * reserve/commit, 27-35 GiB/s submit, pass to pass; from a DRAM-resident
