@@ -223,10 +223,10 @@ int sha1chunk_synth_fill_ragged_async(void *d_base, const uint64_t *d_offsets,
  * NUMA node (SHA1CHUNK_NUMA=off: anywhere); HIP's pinned allocation puts the
  * ring's pages on that node already (measured, every page).
  * Measured on 16384 x 512 KiB host chunks from 4 receive threads on the
- * GPU's node, pieces copied from a cache-resident source: 44-47 GiB/s
- * reserve/commit, 27-35 GiB/s submit, pass to pass; from a DRAM-resident
- * source reserve/commit swings 37-47 GiB/s with the host's memory traffic
- * (profiles/vq_reps_d*.jsonl, bench_r06i*.log). */
+ * GPU's node, one per L3 domain, pieces copied from a cache-resident
+ * source: 45-48 GiB/s reserve/commit and submit alike, pass to pass, 0.88x
+ * the PCIe copy rate; the same from a DRAM-resident source (DESIGN.md
+ * section 6, profiles/vq_l3b.jsonl, bench_r06k*.log). */
 typedef struct sha1chunk_vq sha1chunk_vq;
 /* NULL on failure (sha1chunk_last_error() says why). */
 sha1chunk_vq *sha1chunk_vq_create(size_t batch, uint32_t max_chunk_len);
