@@ -8,6 +8,7 @@
 set -u
 TAG=${TAG:-fixed_ab}
 REPS=${REPS:-2}
+CHUNKS=${CHUNKS:-131072}
 AB_ENV=${AB_ENV:-SHA1CHUNK_LAYOUT_SORTED=0}
 export TMPDIR=/tmp
 mkdir -p gpurun_out/$TAG
@@ -16,7 +17,7 @@ for r in $(seq 1 "$REPS"); do
     for lay in arrival sorted; do
       d=gpurun_out/$TAG/${v}_${lay}_$r
       if [ $v = old ]; then envs="$AB_ENV"; else envs="SHA1CHUNK_AB_NONE=1"; fi
-      env $envs timeout -k 10 200 rocprofv3 --kernel-trace -d $d -o run -- python3 tools/mixed_bench.py --chunks 131072 \
+      env $envs timeout -k 10 200 rocprofv3 --kernel-trace -d $d -o run -- python3 tools/mixed_bench.py --chunks $CHUNKS \
         --modes auto --reps 5 --b2b 5 --layout $lay > $d.log 2>&1 || { echo "fail $d"; exit 1; }
       python3 tools/fixed_cost.py $(find $d -name '*.db' | head -n 1) > $d.jsonl
       python3 - "$d.jsonl" "$v" "$lay" <<'PY'
