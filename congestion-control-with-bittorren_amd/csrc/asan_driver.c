@@ -47,6 +47,20 @@ static uint8_t next_byte(void) {
 
 int main(void) {
     CHECK(sha1chunk_device_count() > 0, "no device: %s", sha1chunk_last_error());
+    /* receive-thread placement: the L3 domains of the GPU's node, round robin */
+    {
+        unsigned char m0[128], m[256];
+        unsigned nd = 0, nd2 = 0;
+        const int c0 = sha1chunk_receive_cpus(0, 0, m0, sizeof m0, &nd);
+        CHECK(c0 > 0 && nd > 0, "receive_cpus: %d %s", c0, sha1chunk_last_error());
+        for (unsigned s = 1; s <= 2 * nd && c0 > 0 && nd > 0; ++s) {
+            const int c = sha1chunk_receive_cpus(0, s, m, sizeof m, &nd2);  /* a longer mask: zero-filled */
+            CHECK(c > 0 && nd2 == nd, "receive_cpus slot %u", s);
+            for (size_t i = 128; i < sizeof m; ++i) CHECK(m[i] == 0, "receive_cpus tail byte %zu", i);
+            CHECK((s % nd == 0) == !memcmp(m, m0, sizeof m0), "receive_cpus round robin %u", s);
+        }
+        CHECK(sha1chunk_receive_cpus(0, 0, m, 64, NULL) == SHA1CHUNK_EINVAL, "receive_cpus short mask");
+    }
     /* NIST "abc" (sha.c:32-38) through shahash and the streaming trio */
     static const uint8_t abc_want[20] = {0xa9, 0x99, 0x3e, 0x36, 0x47, 0x06, 0x81, 0x6a, 0xba, 0x3e,
                                          0x25, 0x71, 0x78, 0x50, 0xc2, 0x6c, 0x9c, 0xd0, 0xd8, 0x9d};

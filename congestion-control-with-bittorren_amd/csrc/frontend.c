@@ -31,6 +31,7 @@
 #include <dlfcn.h>
 #include <errno.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -87,6 +88,7 @@ static int fail(int code, const char *fmt, ...) {
     X(int, device_count, (void))                                                                  \
     X(int, set_device, (int))                                                                     \
     X(int, device_pci_bus_id, (int, char *, size_t))                                              \
+    X(int, receive_cpus, (int, unsigned, void *, size_t, unsigned *))                             \
     X(const char *, last_error, (void))
 
 #define BE_FIELD(ret, name, args) ret(*name) args;
@@ -365,6 +367,16 @@ FE_API int sha1chunk_device_pci_bus_id(int device, char *buf, size_t len) {
     int rc = backend();
     if (rc) return rc;
     if ((rc = BE.device_pci_bus_id(device, buf, len)) < 0) fail(rc, "%s", BE.last_error());
+    return rc;
+}
+
+FE_API int sha1chunk_receive_cpus(int device, unsigned slot, void *mask, size_t len, unsigned *domains) {
+    if (!mask) return fail(SHA1CHUNK_EINVAL, "null mask");
+    if (len < sizeof(cpu_set_t)) return fail(SHA1CHUNK_EINVAL, "mask of %zu bytes, a cpu_set_t needs %zu", len,
+                                             sizeof(cpu_set_t));
+    int rc = backend();
+    if (rc) return rc;
+    if ((rc = BE.receive_cpus(device, slot, mask, len, domains)) < 0) fail(rc, "%s", BE.last_error());
     return rc;
 }
 

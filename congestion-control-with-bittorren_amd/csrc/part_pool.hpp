@@ -15,6 +15,7 @@
 #include <mutex>
 #include <pthread.h>
 #include <sched.h>
+#include <string>
 #include <thread>
 #include <vector>
 
@@ -163,6 +164,33 @@ inline int cpus_from_list(const char* list, const cpu_set_t& allowed, cpu_set_t*
         if (p) ++p;
     }
     return CPU_COUNT(out);
+}
+
+// The L3 domains (CPUs that share a last-level cache: a CCD on the EPYC
+// hosts of the MI355X boxes) of the CPUs in `within`, in CPU order, into
+// *out; list_of(cpu) gives a CPU's sysfs shared_cpu_list ("0-7,128-135\n"),
+// empty if unknown.  A CPU whose list is unknown or leaves it out is a
+// domain of its own; a CPU lands in the first domain that names it.  The
+// runtime hands one domain per receive thread (sha1chunk_receive_cpus).
+template <class ListOf>
+inline int l3_domains(const cpu_set_t& within, std::vector<cpu_set_t>* out, ListOf list_of) {
+    out->clear();
+    cpu_set_t seen;
+    CPU_ZERO(&seen);
+    for (int c = 0; c < CPU_SETSIZE; ++c) {
+        if (!CPU_ISSET(c, &within) || CPU_ISSET(c, &seen)) continue;
+        cpu_set_t d;
+        const std::string list = list_of(c);
+        if (cpus_from_list(list.c_str(), within, &d) == 0 || !CPU_ISSET(c, &d)) {
+            CPU_ZERO(&d);
+            CPU_SET(c, &d);
+        }
+        for (int x = 0; x < CPU_SETSIZE; ++x)
+            if (CPU_ISSET(x, &d) && CPU_ISSET(x, &seen)) CPU_CLR(x, &d);
+        CPU_OR(&seen, &seen, &d);
+        out->push_back(d);
+    }
+    return static_cast<int>(out->size());
 }
 
 // memcpy split over a pool (pieces of >= 64 KiB)

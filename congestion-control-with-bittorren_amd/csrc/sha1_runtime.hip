@@ -43,15 +43,49 @@
 namespace {
 using s1host::PartPool;
 
-// Host CPUs near HIP device `id`: the CPUs of its NUMA node (the numa_node
-// of its PCI device) within this process's affinity mask.  The library's
-// helper threads -- the verify queue's copies into the pinned ring, the
-// pageable-batch packing, the file pipeline's preads into pinned slots --
-// run there, beside the pinned memory they write (hipHostMalloc already
-// places it on the GPU's node: profiles/vq_place_r06*.jsonl) and the GPU that
-// reads it.  SHA1CHUNK_NUMA=off (or 0) leaves them to the scheduler.
-// nullptr: no placement (off, one node, node unknown, or none of its CPUs
-// allowed, or fewer than four).
+// First line of a sysfs file ("" if it cannot be read).
+std::string sysfs_line(const char* path) {
+    char buf[4096] = {0};
+    if (FILE* f = fopen(path, "r")) {
+        if (!fgets(buf, sizeof buf, f)) buf[0] = 0;
+        fclose(f);
+    }
+    return buf;
+}
+
+// The CPUs of HIP device `id`'s NUMA node (the numa_node of its PCI device)
+// within `allowed`, into *out; their count, 0 when the node is unknown.
+int device_node_cpus(int id, const cpu_set_t& allowed, cpu_set_t* out) {
+    CPU_ZERO(out);
+    char bdf[64] = {0};
+    if (hipDeviceGetPCIBusId(bdf, sizeof bdf, id) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    for (char* c = bdf; *c; ++c) *c = static_cast<char>(tolower(static_cast<unsigned char>(*c)));
+    char path[160];
+    snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bdf);
+    const std::string nl = sysfs_line(path);
+    const int node = nl.empty() ? -1 : atoi(nl.c_str());
+    if (node < 0) return 0;
+    snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
+    return s1host::cpus_from_list(sysfs_line(path).c_str(), allowed, out);
+}
+
+bool numa_off() {
+    const char* e = getenv("SHA1CHUNK_NUMA");
+    return e && (!strcmp(e, "off") || !strcmp(e, "0"));
+}
+
+// Host CPUs near HIP device `id`: the CPUs of its NUMA node within this
+// process's affinity mask.  The library's helper threads -- the pageable-
+// batch packing, the file pipeline's preads into pinned slots, the verify
+// queue's split copies when asked for (SHA1CHUNK_VQ_THREADS) -- run there,
+// beside the pinned memory they write (hipHostMalloc already places it on
+// the GPU's node: profiles/vq_place_r06*.jsonl) and the GPU that reads it.
+// SHA1CHUNK_NUMA=off (or 0) leaves them to the scheduler.  nullptr: no
+// placement (off, one node, node unknown, or none of its CPUs allowed, or
+// fewer than four).
 const cpu_set_t* near_cpus(int id) {
     struct Near {
         std::once_flag once;
@@ -62,38 +96,44 @@ const cpu_set_t* near_cpus(int id) {
     if (id < 0 || id >= 64) return nullptr;
     Near& n = near[id];
     std::call_once(n.once, [&] {
-        const char* e = getenv("SHA1CHUNK_NUMA");
-        if (e && (!strcmp(e, "off") || !strcmp(e, "0"))) return;
-        char bdf[64] = {0};
-        if (hipDeviceGetPCIBusId(bdf, sizeof bdf, id) != hipSuccess) {
-            (void)hipGetLastError();
-            return;
-        }
-        for (char* c = bdf; *c; ++c) *c = static_cast<char>(tolower(static_cast<unsigned char>(*c)));
-        int node = -1;
-        char path[160];
-        snprintf(path, sizeof path, "/sys/bus/pci/devices/%s/numa_node", bdf);
-        if (FILE* f = fopen(path, "r")) {
-            if (fscanf(f, "%d", &node) != 1) node = -1;
-            fclose(f);
-        }
-        if (node < 0) return;
-        char list[4096] = {0};
-        snprintf(path, sizeof path, "/sys/devices/system/node/node%d/cpulist", node);
-        if (FILE* f = fopen(path, "r")) {
-            if (!fgets(list, sizeof list, f)) list[0] = 0;
-            fclose(f);
-        }
+        if (numa_off()) return;
         cpu_set_t allowed, mine;
         if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return;
         // nothing to gain when every allowed CPU is on this node already,
         // and no piling of a pool's helpers onto fewer than kMinNearCpus
         constexpr int kMinNearCpus = 4;
-        if (s1host::cpus_from_list(list, allowed, &mine) < kMinNearCpus || CPU_EQUAL(&mine, &allowed)) return;
+        if (device_node_cpus(id, allowed, &mine) < kMinNearCpus || CPU_EQUAL(&mine, &allowed)) return;
         n.set = mine;
         n.ok = true;
     });
     return n.ok ? &n.set : nullptr;
+}
+
+// Receive-thread placement (sha1chunk_receive_cpus): the L3 domains of
+// HIP device `id`'s node's allowed CPUs, in CPU order (of every allowed CPU
+// under SHA1CHUNK_NUMA=off or when the node is unknown), once per device.
+// One receive thread per domain kept `submit` at 27.7-29.6 GiB/s where
+// threads floating over the node gave 23.8-36.2 (profiles/vq_l3.jsonl).
+const std::vector<cpu_set_t>& receive_domains(int id) {
+    struct Dom {
+        std::once_flag once;
+        std::vector<cpu_set_t> dom;
+    };
+    static Dom doms[64];
+    static const std::vector<cpu_set_t> none;
+    if (id < 0 || id >= 64) return none;
+    Dom& d = doms[id];
+    std::call_once(d.once, [&] {
+        cpu_set_t allowed, base;
+        if (sched_getaffinity(0, sizeof allowed, &allowed) != 0) return;
+        if (numa_off() || device_node_cpus(id, allowed, &base) == 0) base = allowed;
+        s1host::l3_domains(base, &d.dom, [](int cpu) {
+            char path[128];
+            snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", cpu);
+            return sysfs_line(path);
+        });
+    });
+    return d.dom;
 }
 using s1host::pool_copy;
 thread_local std::string t_err;
@@ -717,6 +757,21 @@ int s1be_device_pci_bus_id(int device, char* buf, size_t len) {
     if (len > static_cast<size_t>(INT32_MAX)) len = INT32_MAX;
     HIP_TRY(hipDeviceGetPCIBusId(buf, static_cast<int>(len), g_dev[device].id));
     return SHA1CHUNK_OK;
+}
+
+// The CPUs for receive thread `slot` of device `device` (L3 domain slot mod
+// their count; receive_domains), as a cpu_set_t of `len` >= its size bytes.
+int s1be_receive_cpus(int device, unsigned slot, void* mask, size_t len, unsigned* domains) {
+    const int n = device_count();
+    if (n <= 0) return fail(SHA1CHUNK_ENODEV, "%s", g_probe_err.c_str());
+    if (device < 0 || device >= n) return fail(SHA1CHUNK_EINVAL, "device %d of %d", device, n);
+    const std::vector<cpu_set_t>& dom = receive_domains(g_dev[device].id);
+    if (dom.empty()) return fail(SHA1CHUNK_EINVAL, "no CPU of this process's affinity mask found");
+    const cpu_set_t& d = dom[slot % dom.size()];
+    memset(mask, 0, len);
+    memcpy(mask, &d, sizeof d);
+    if (domains) *domains = static_cast<unsigned>(dom.size());
+    return CPU_COUNT(&d);
 }
 
 int s1be_hash_device_async(const void* d_base, const uint64_t* d_offsets,

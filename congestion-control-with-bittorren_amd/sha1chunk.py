@@ -112,6 +112,7 @@ _SIGNATURES = [
     ("sha1chunk_set_device", C.c_int, [C.c_int]),
     ("sha1chunk_get_device", C.c_int, []),
     ("sha1chunk_device_pci_bus_id", C.c_int, [C.c_int, C.c_char_p, C.c_size_t]),
+    ("sha1chunk_receive_cpus", C.c_int, [C.c_int, C.c_uint, _vp, C.c_size_t, C.POINTER(C.c_uint)]),
     ("sha1chunk_last_error", C.c_char_p, []),
     ("sha1chunk_version", C.c_char_p, []),
 ]
@@ -167,6 +168,15 @@ def device_pci_bus_id(dev: int) -> str:
     buf = C.create_string_buffer(64)
     _check(lib().sha1chunk_device_pci_bus_id(dev, buf, len(buf)), "sha1chunk_device_pci_bus_id")
     return buf.value.decode()
+
+
+def receive_cpus(dev: int, slot: int) -> tuple[list[int], int]:
+    """The CPUs for receive thread `slot` of a verify queue on `dev` (one L3
+    domain of the device's NUMA node) and the number of such domains."""
+    mask = (C.c_uint8 * 128)()  # a glibc cpu_set_t: 1024 CPUs
+    doms = C.c_uint(0)
+    _check(lib().sha1chunk_receive_cpus(dev, slot, mask, len(mask), C.byref(doms)), "sha1chunk_receive_cpus")
+    return [8 * i + b for i in range(len(mask)) for b in range(8) if mask[i] >> b & 1], doms.value
 
 
 def version() -> str:

@@ -121,6 +121,22 @@ def test_verify_queue_without_device_fails_loudly(pkg):
         pkg.VerifyQueue(batch=16)
 
 
+def test_receive_cpus_checks_its_mask(pkg, built):
+    """sha1chunk_receive_cpus (include/sha1chunk.h): a NULL or short mask is
+    refused before any device work; without a device it fails loudly."""
+    L = pkg.sha1chunk.lib()
+    doms = C.c_uint(7)
+    assert L.sha1chunk_receive_cpus(0, 0, None, 128, C.byref(doms)) == pkg.sha1chunk.EINVAL
+    short = (C.c_uint8 * 64)()
+    assert L.sha1chunk_receive_cpus(0, 0, short, 64, C.byref(doms)) == pkg.sha1chunk.EINVAL
+    assert b"cpu_set_t" in L.sha1chunk_last_error()
+    assert doms.value == 7  # untouched on failure
+    if not _has_device(pkg):
+        with pytest.raises(pkg.Sha1ChunkError) as ei:
+            pkg.sha1chunk.receive_cpus(0, 0)
+        assert ei.value.code == pkg.sha1chunk.ENODEV
+
+
 def test_python_mirror_names(pkg):
     for name in ("shahash", "binary2hex", "hex2binary", "make_chunks", "get_chunk_hash",
                  "verify_hash", "SHA1"):

@@ -145,6 +145,7 @@ def test_chunk_file_readers_under_asan_ubsan(tmp_path):
 _POOL_DRV = r'''
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 #include <vector>
 #include <pthread.h>
 #include <sched.h>
@@ -185,6 +186,45 @@ int main() {
         bad += s1host::cpus_from_list("x,5,,7-,9-8,12-13", all, &out) != 4;  // 5, 7, 12, 13
         for (int c : {5, 7, 12, 13}) bad += !CPU_ISSET(c, &out);
         bad += s1host::cpus_from_list("", all, &out) != 0;
+    }
+    // L3 domains (sha1chunk_receive_cpus): four 4-core CCDs with SMT
+    // siblings at +16, CPU 4's list unreadable, CPU 8's naming a domain that
+    // leaves CPU 8 out, CPUs 20-31 not allowed
+    {
+        cpu_set_t within;
+        CPU_ZERO(&within);
+        for (int c = 0; c < 20; ++c) CPU_SET(c, &within);
+        auto list_of = [](int c) -> std::string {
+            if (c == 4) return "";
+            if (c == 8) return "10-11";
+            const int ccd = (c % 16) / 4;
+            char b[64];
+            std::snprintf(b, sizeof b, "%d-%d,%d-%d\n", 4 * ccd, 4 * ccd + 3, 16 + 4 * ccd, 19 + 4 * ccd);
+            return b;
+        };
+        std::vector<cpu_set_t> dom;
+        const int n = s1host::l3_domains(within, &dom, list_of);
+        // {0-3,16-19} {4} {5,6,7} {8} {9,10,11} {12-15}
+        bad += n != 6;
+        if (n == 6) {
+            bad += CPU_COUNT(&dom[0]) != 8 || !CPU_ISSET(16, &dom[0]) || !CPU_ISSET(19, &dom[0]);
+            bad += CPU_COUNT(&dom[1]) != 1 || !CPU_ISSET(4, &dom[1]);
+            bad += CPU_COUNT(&dom[2]) != 3 || CPU_ISSET(4, &dom[2]);
+            bad += CPU_COUNT(&dom[3]) != 1 || !CPU_ISSET(8, &dom[3]);
+            bad += CPU_COUNT(&dom[4]) != 3 || CPU_ISSET(8, &dom[4]) || !CPU_ISSET(9, &dom[4]);
+            bad += CPU_COUNT(&dom[5]) != 4 || !CPU_ISSET(12, &dom[5]);
+        }
+        cpu_set_t u;
+        CPU_ZERO(&u);
+        int total = 0;
+        for (auto& d : dom) {
+            CPU_OR(&u, &u, &d);
+            total += CPU_COUNT(&d);
+        }
+        bad += !CPU_EQUAL(&u, &within) || total != 20;  // a partition of `within`
+        cpu_set_t none;
+        CPU_ZERO(&none);
+        bad += s1host::l3_domains(none, &dom, list_of) != 0;
     }
     // helpers pinned to a CPU set run their parts there (the caller's own
     // parts run wherever the caller runs)

@@ -31,9 +31,9 @@
  * (within this process's affinity mask) and has each producer write its own
  * source chunks there (first touch), as a NIC-local receive thread would;
  * --pin none leaves placement to the scheduler.  --pin l3 binds producer t
- * to the t-th L3 domain (the CPUs sharing cache/index3) of the GPU node's
- * CPUs, round robin: one receive thread per CCD, each with its own L3 and
- * link to the memory controllers.
+ * where sha1chunk_receive_cpus(dev, t) says: the t-th L3 domain (CPUs that
+ * share cache/index3) of the GPU node's CPUs, round robin -- one receive
+ * thread per CCD, each with its own L3 and link to the memory controllers.
  */
 #define _GNU_SOURCE
 #include <ctype.h>
@@ -159,37 +159,6 @@ static int node_cpus(int node, cpu_set_t *out) {
     return CPU_COUNT(out);
 }
 
-/* The L3 domains of the CPUs in `within`, in CPU order (at most maxd). */
-static int l3_domains(const cpu_set_t *within, cpu_set_t *dom, int maxd) {
-    int nd = 0;
-    cpu_set_t seen;
-    CPU_ZERO(&seen);
-    for (int c = 0; c < CPU_SETSIZE && nd < maxd; ++c) {
-        if (!CPU_ISSET(c, within) || CPU_ISSET(c, &seen)) continue;
-        char path[128], buf[4096];
-        snprintf(path, sizeof path, "/sys/devices/system/cpu/cpu%d/cache/index3/shared_cpu_list", c);
-        FILE *f = fopen(path, "r");
-        if (!f) return 0;
-        if (!fgets(buf, sizeof buf, f)) buf[0] = 0;
-        fclose(f);
-        CPU_ZERO(&dom[nd]);
-        for (char *tok = strtok(buf, ",\n"); tok; tok = strtok(NULL, ",\n")) {
-            int a, b;
-            const int k = sscanf(tok, "%d-%d", &a, &b);
-            if (k < 1) continue;
-            if (k == 1) b = a;
-            for (int x = a; x <= b && x < CPU_SETSIZE; ++x)
-                if (CPU_ISSET(x, within)) {
-                    CPU_SET(x, &dom[nd]);
-                    CPU_SET(x, &seen);
-                }
-        }
-        CPU_SET(c, &seen);
-        if (CPU_COUNT(&dom[nd]) > 0) ++nd;
-    }
-    return nd;
-}
-
 /* cgroup CPU throttling counters (v2 cpu.stat; v1 cpu/cpu.stat, ns) */
 static void cg_throttle(long long *nr, long long *usec) {
     *nr = *usec = -1;
@@ -224,7 +193,7 @@ static struct {
     int pin;           /* 1: producers on the GPU node's CPUs, source chunks first-touched there */
     int local_src;     /* producers write their own source chunks */
     cpu_set_t pin_set;
-    int ndom;          /* --pin l3: producer t on dom[t % ndom] */
+    int ndom;          /* --pin l3: L3 domains; producer t on dom[t] (sha1chunk_receive_cpus) */
     cpu_set_t dom[64];
     int cpu0[64], cpu1[64];
     int own_node[64]; /* submit: the node of each producer's session buffer (-1 unknown) */
@@ -263,7 +232,7 @@ static void fill(uint8_t *dst, const uint8_t *src) {
 
 static void *producer(void *arg) {
     const int t = (int)(intptr_t)arg;
-    if (B.pin) (void)sched_setaffinity(0, sizeof B.pin_set, B.ndom ? &B.dom[t % B.ndom] : &B.pin_set);
+    if (B.pin) (void)sched_setaffinity(0, sizeof B.pin_set, B.ndom ? &B.dom[t % 64] : &B.pin_set);
     if (B.local_src)
         for (size_t c = (size_t)t; c < B.distinct; c += (size_t)B.threads)
             synth_chunk(B.src + c * (size_t)L512, c);
@@ -356,7 +325,16 @@ int main(int argc, char **argv) {
     const int gnode = gpu_node(bdf, sizeof bdf);
     const int ncpu_pin = node_cpus(gnode, &B.pin_set);
     B.pin = strcmp(pin, "none") && ncpu_pin > 0;
-    B.ndom = B.pin && !strcmp(pin, "l3") ? l3_domains(&B.pin_set, B.dom, 64) : 0;
+    B.ndom = 0;
+    if (B.pin && !strcmp(pin, "l3")) /* the library's placement for receive thread t */
+        for (int t = 0; t < B.threads && t < 64; ++t) {
+            unsigned nd = 0;
+            if (sha1chunk_receive_cpus(sha1chunk_get_device(), (unsigned)t, &B.dom[t], sizeof B.dom[t], &nd) <= 0) {
+                fprintf(stderr, "vq_zc_bench: receive_cpus: %s\n", sha1chunk_last_error());
+                return 2;
+            }
+            B.ndom = (int)nd;
+        }
     /* producer t reads chunks c = t mod threads only when threads divides distinct */
     B.local_src = B.pin && B.distinct % (size_t)B.threads == 0;
     const char *src_touch = B.local_src ? "producers" : "main thread";
