@@ -120,10 +120,24 @@ _SIGNATURES = [
 _lib: C.CDLL | None = None
 
 
+def _one_hip_runtime() -> None:
+    """One HIP runtime per process.  The library's backend binds to the HIP
+    runtime already loaded in the process (same soname); loaded before
+    PyTorch's, it brings /opt/rocm's own and the process then holds two, and
+    torch sees no device (tools/order_probe.py, profiles/order_probe_r06.log).
+    So where PyTorch is installed its runtime is initialised first."""
+    try:
+        import torch
+    except ImportError:
+        return
+    torch.cuda.is_available()
+
+
 def lib() -> C.CDLL:
     """Load libsha1chunk.so (raises if it was never built)."""
     global _lib
     if _lib is None:
+        _one_hip_runtime()
         if not os.path.exists(LIB_PATH):
             raise FileNotFoundError(
                 f"{LIB_PATH} is missing: build it with __graft_entry__.build() or "
